@@ -1,0 +1,210 @@
+/*
+ * lz4e.h -- C ABI of the MI355X-native LZ4E scatter-gather block codec.
+ *
+ * Drop-in boundary for the reference's two exported symbols:
+ *   LZ4E_compress_default  <- /root/reference/lz4e/include/lz4e.h:47-48
+ *                             (definition lz4e/lz4e_compress.c:563-569)
+ *   LZ4E_decompress_safe   <- /root/reference/lz4e/include/lz4e.h:50-51
+ *                             (definition lz4e/lz4e_decompress.c:462-470)
+ * plus the sizing macros of lz4e/include/lz4e.h:9-28,53-55 and the
+ * LZ4E_stream_t work-memory layout of lz4e/include/lz4e.h:33-45.
+ *
+ * Both single-call entry points run on the GPU (gfx950): the host shim
+ * gathers the bio_vec segments into pinned staging, copies them to HBM,
+ * launches the hand-written HIP kernel and scatters the frame back into the
+ * destination bio_vecs.  There is no CPU codec behind these symbols; when no
+ * GPU is usable they fail (compress returns 0, decompress returns a negative
+ * value) and lz4e_last_error() says why.
+ *
+ * The batched lz4e_*_batch_* entry points are the throughput path: many
+ * independent blocks per launch, device-resident buffers, caller's stream.
+ *
+ * Plain C, no torch types.  All sizes are bytes.
+ */
+#ifndef LZ4E_AMD_H
+#define LZ4E_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Userspace view of the kernel block-layer SG types (doc/API.md:47-82).     */
+/* ------------------------------------------------------------------------ */
+#ifndef LZ4E_HAVE_KERNEL_BVEC
+/*
+ * A page frame.  Userspace model: page_address(p) == (char *)p and a
+ * multi-page bvec covers physically contiguous pages, so byte k of a bvec
+ * lives at (char *)bv_page + bv_offset + k.
+ */
+struct page;
+
+struct bio_vec {
+	struct page *bv_page;   /* first page the segment lives on        */
+	unsigned int bv_len;    /* segment length in bytes                */
+	unsigned int bv_offset; /* offset of the segment inside bv_page   */
+};
+
+struct bvec_iter {
+	uint64_t bi_sector;        /* unused by the codec                  */
+	unsigned int bi_size;      /* residual bytes                       */
+	unsigned int bi_idx;       /* current index into the bio_vec array */
+	unsigned int bi_bvec_done; /* bytes done in the current bio_vec    */
+};
+#endif
+
+#define LZ4E_PAGE_SIZE 4096u
+#ifndef BIO_MAX_VECS
+#define BIO_MAX_VECS 256
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Sizing macros (values fixed by the reference: lz4e/include/lz4e.h)        */
+/* ------------------------------------------------------------------------ */
+#define LZ4E_NAME "lz4e"
+#define LZ4E_ACCELERATION_DEFAULT 1
+#define LZ4E_MEMORY_USAGE 14
+#define LZ4E_HASHLOG (LZ4E_MEMORY_USAGE - 2)
+#define LZ4E_HASH_SIZE_U32 (1 << LZ4E_HASHLOG)
+#define LZ4E_HASH_SIZE_U64 (LZ4E_HASH_SIZE_U32 >> 1)
+#define LZ4E_BV_ITER_SIZE_U64 (BIO_MAX_VECS >> 1)
+#define LZ4E_STREAMSIZE_U64 (LZ4E_HASH_SIZE_U64 + LZ4E_BV_ITER_SIZE_U64 + 4)
+#define LZ4E_STREAMSIZE (LZ4E_STREAMSIZE_U64 * sizeof(unsigned long long))
+#define LZ4E_MEM_COMPRESS LZ4E_STREAMSIZE /* 17440 bytes */
+
+#define LZ4E_MAX_INPUT_SIZE 0x7E000000 /* 2 113 929 216 bytes */
+#define LZ4E_COMPRESSBOUND(isize)                                        \
+	((unsigned int)(isize) > (unsigned int)LZ4E_MAX_INPUT_SIZE ? 0 :  \
+	 (isize) + ((isize) / 255) + 16)
+
+#ifndef LZ4E_DISTANCE_MAX
+#define LZ4E_DISTANCE_MAX 65535
+#endif
+
+/* Work-memory layout (same size/shape as the reference's LZ4E_stream_t). */
+typedef struct {
+	uint32_t bvIterSize[BIO_MAX_VECS];
+	uint32_t hashTable[LZ4E_HASH_SIZE_U32];
+	uint32_t currentOffset;
+	uint32_t initCheck;
+	const uint8_t *dictionary;
+	uint8_t *bufferStart;
+	uint32_t dictSize;
+} LZ4E_stream_t_internal;
+
+typedef union {
+	unsigned long long table[LZ4E_STREAMSIZE_U64];
+	LZ4E_stream_t_internal internal_donotuse;
+} LZ4E_stream_t;
+
+/* Hash-table address classes chosen from the SG layout
+ * (lz4e/include/lz4e_defs.h:689, rules lz4e/lz4e_compress.c:184-211). */
+#define LZ4E_TABLE_BYU16 1
+#define LZ4E_TABLE_BYU32 3
+#define LZ4E_TABLE_BYU64 7
+
+/* ------------------------------------------------------------------------ */
+/* Reference entry points (drop-in).                                         */
+/* ------------------------------------------------------------------------ */
+
+/*
+ * Compress srcIter->bi_size bytes read through the bio_vec list `src`
+ * (starting at *srcIter) into one raw LZ4 block written through `dst`
+ * starting at *dstIter; dstIter->bi_size is the output capacity.
+ * Returns the block size, or 0 on failure (input too large, more than
+ * BIO_MAX_VECS segments, output capacity too small, or no usable GPU).
+ * On success *dstIter is advanced by (ret - last literal run) and *srcIter
+ * to the last position the match finder visited, like the reference.
+ * `wrkmem` must point to LZ4E_MEM_COMPRESS bytes; it is zeroed on entry
+ * (the match finder's state itself lives in GPU LDS).
+ * Replaces lz4e/lz4e_compress.c:563.
+ */
+int LZ4E_compress_default(const struct bio_vec *src, struct bio_vec *dst,
+			  struct bvec_iter *srcIter, struct bvec_iter *dstIter,
+			  void *wrkmem);
+
+/*
+ * Safe full-block decode of `compressedSize` bytes at `source` into at most
+ * `maxDecompressedSize` bytes at `dest` (contiguous host buffers).
+ * Returns the number of bytes written, or -(input position of the error)-1.
+ * Replaces lz4e/lz4e_decompress.c:462 (and, with the same signature, the
+ * kernel LZ4_decompress_safe call at lz4e_bdev/lz4e_chunk.c:125).
+ */
+int LZ4E_decompress_safe(const char *source, char *dest, int compressedSize,
+			 int maxDecompressedSize);
+
+/* ------------------------------------------------------------------------ */
+/* Extensions                                                                */
+/* ------------------------------------------------------------------------ */
+
+/* Table class of an SG source (1/3/7), or 0 when it spans more than
+ * BIO_MAX_VECS segments.  Only meaningful for bi_size >= 13 (smaller inputs
+ * never consult the table).  Rules of lz4e/lz4e_compress.c:184-211. */
+int lz4e_sg_table_type(const struct bio_vec *src, const struct bvec_iter *it);
+
+/* Human-readable reason for the last failure on this thread ("" if none). */
+const char *lz4e_last_error(void);
+
+/* 1 if a gfx950 device is usable by the library, else 0. */
+int lz4e_gpu_available(void);
+
+/*
+ * One SG compress request of a host batch.  Same meaning as the arguments
+ * of LZ4E_compress_default; `ret` receives its return value.  The
+ * iterators are updated exactly like the single-call form.
+ */
+struct lz4e_sg_request {
+	const struct bio_vec *src;
+	struct bio_vec *dst;
+	struct bvec_iter *srcIter;
+	struct bvec_iter *dstIter;
+	int ret;
+};
+
+/* Compress `n` independent SG requests with one gather, one H2D copy, one
+ * kernel launch, one D2H copy and one scatter.  Returns the number of
+ * requests that succeeded (ret > 0), or -1 when no GPU is usable. */
+int lz4e_compress_sg_batch(struct lz4e_sg_request *reqs, int n);
+
+/* Decompress `n` independent contiguous host blocks (src[i], csize[i]) into
+ * (dst[i], cap[i]); ret[i] receives LZ4E_decompress_safe's value.  Returns
+ * the number of blocks with ret >= 0, or -1 when no GPU is usable. */
+int lz4e_decompress_batch(const char *const *src, const int *csize,
+			  char *const *dst, const int *cap, int *ret, int n);
+
+/*
+ * Device-resident batch compress (the throughput path).  All pointers are
+ * device (HBM) pointers; `stream` is a hipStream_t (NULL = default stream).
+ * Block i reads src_len[i] bytes at src + src_off[i], uses table class
+ * table_type[i] (1/3/7, from lz4e_sg_table_type of its SG layout) and writes
+ * at most dst_cap[i] bytes at dst + dst_off[i]; ret[i] receives the block
+ * size or 0.  `aux` (nullable, 2 words per block) receives
+ * {final src position, last literal run} for iterator post-state.
+ * `max_len` bounds src_len[] (it selects the LDS staging mode).
+ * Returns 0 on a successful launch, else a negative error.
+ */
+int lz4e_compress_batch_dev(const uint8_t *src, const uint64_t *src_off,
+			    const uint32_t *src_len, const uint8_t *table_type,
+			    uint8_t *dst, const uint64_t *dst_off,
+			    const uint32_t *dst_cap, int32_t *ret, uint32_t *aux,
+			    uint32_t nblocks, uint32_t max_len, void *stream);
+
+/*
+ * Device-resident batch decompress.  Block i decodes src_len[i] bytes at
+ * src + src_off[i] into at most dst_cap[i] bytes at dst + dst_off[i];
+ * ret[i] receives LZ4E_decompress_safe's return value.
+ * Returns 0 on a successful launch, else a negative error.
+ */
+int lz4e_decompress_batch_dev(const uint8_t *src, const uint64_t *src_off,
+			      const int32_t *src_len, uint8_t *dst,
+			      const uint64_t *dst_off, const int32_t *dst_cap,
+			      int32_t *ret, uint32_t nblocks, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LZ4E_AMD_H */

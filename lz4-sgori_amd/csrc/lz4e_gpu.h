@@ -1,0 +1,43 @@
+// lz4e_gpu.h -- internal (C++) launch interface of the gfx950 LZ4E kernels.
+// The public C ABI is include/lz4e.h; lz4e_host.hip maps it onto these.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lz4e {
+
+// Largest block whose bytes are staged in LDS by the compressor (64 KiB
+// block + 16 KiB table = half a CU's LDS, two blocks per CU).
+constexpr uint32_t kMaxLdsInput = 65536;
+
+struct CompressBatch {
+    const uint8_t* src;
+    const uint64_t* src_off;
+    const uint32_t* src_len;
+    const uint8_t* table_type;
+    uint8_t* dst;
+    const uint64_t* dst_off;
+    const uint32_t* dst_cap;
+    int32_t* ret;
+    uint32_t* aux;  // nullable, 2 words per block
+    uint32_t nblocks;
+    uint32_t max_len;
+};
+
+struct DecompressBatch {
+    const uint8_t* src;
+    const uint64_t* src_off;
+    const int32_t* src_len;
+    uint8_t* dst;
+    const uint64_t* dst_off;
+    const int32_t* dst_cap;
+    int32_t* ret;
+    uint32_t nblocks;
+};
+
+uint32_t compress_lds_bytes(uint32_t max_len, bool lds_input);
+hipError_t launch_compress(const CompressBatch& a, hipStream_t stream);
+hipError_t launch_decompress(const DecompressBatch& a, hipStream_t stream);
+
+}  // namespace lz4e

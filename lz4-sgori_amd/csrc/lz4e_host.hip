@@ -1,0 +1,423 @@
+// lz4e_host.hip -- C ABI of include/lz4e.h on top of the gfx950 kernels.
+//
+// Single-call entry points keep the reference's synchronous, per-request
+// contract (lz4e_bdev/lz4e_chunk.c:139-159 calls LZ4E_compress_default once
+// per WRITE bio): gather the SG segments into pinned staging, one H2D copy,
+// one kernel launch, one D2H copy, scatter into the destination segments.
+// The batched entry points amortise that over many requests; the *_dev
+// forms launch straight on device-resident buffers.
+//
+// There is no CPU codec here: without a usable gfx950 device every entry
+// point fails (compress 0, decompress < 0) and lz4e_last_error() says why.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/lz4e.h"
+#include "lz4e_gpu.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const std::string& s) { g_err = s; }
+
+bool hip_ok(hipError_t e, const char* what) {
+    if (e == hipSuccess) return true;
+    set_err(std::string(what) + ": " + hipGetErrorString(e));
+    return false;
+}
+
+uint32_t bound_of(uint32_t n) { return n > LZ4E_MAX_INPUT_SIZE ? 0u : n + n / 255 + 16; }
+
+uint64_t align16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+
+// Growable device / pinned-host byte buffer.
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool ensure(size_t n) {
+        if (n <= cap) return true;
+        const size_t want = std::max(n, cap * 2);
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        if (!hip_ok(hipMalloc(&p, want), "hipMalloc")) return false;
+        cap = want;
+        return true;
+    }
+};
+
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    bool ensure(size_t n) {
+        if (n <= cap) return true;
+        const size_t want = std::max(n, cap * 2);
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        if (!hip_ok(hipHostMalloc(&p, want, hipHostMallocDefault), "hipHostMalloc")) return false;
+        cap = want;
+        return true;
+    }
+};
+
+// One process-wide context: the device, a stream and staging buffers.
+struct Ctx {
+    std::mutex mu;
+    int state = 0;  // 0 unknown, 1 ok, -1 unusable
+    std::string why;
+    hipStream_t stream = nullptr;
+    DevBuf d_data, d_meta;
+    HostBuf h_data, h_meta;
+
+    bool init() {
+        if (state == 1) return true;
+        if (state == -1) {
+            set_err(why);
+            return false;
+        }
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+            why = "lz4e: no HIP device visible";
+            state = -1;
+            set_err(why);
+            return false;
+        }
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+            std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            why = std::string("lz4e: device is not gfx950 (") + prop.gcnArchName + ")";
+            state = -1;
+            set_err(why);
+            return false;
+        }
+        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
+            why = "lz4e: hipStreamCreate failed";
+            state = -1;
+            set_err(why);
+            return false;
+        }
+        state = 1;
+        return true;
+    }
+};
+
+Ctx& ctx() {
+    static Ctx c;
+    return c;
+}
+
+// ---------------------------------------------------------------------------
+// SG helpers (userspace model of lz4e/include/lz4e_defs.h:115-197)
+// ---------------------------------------------------------------------------
+
+inline const uint8_t* bv_data(const struct bio_vec& b) {
+    return reinterpret_cast<const uint8_t*>(b.bv_page) + b.bv_offset;
+}
+
+// Copy `len` bytes starting at iterator `it` out of the SG list.
+void sg_gather(const struct bio_vec* bv, const struct bvec_iter& it, uint8_t* to, uint32_t len) {
+    uint32_t idx = it.bi_idx, done = it.bi_bvec_done;
+    while (len) {
+        uint32_t take = std::min(bv[idx].bv_len - done, len);
+        std::memcpy(to, bv_data(bv[idx]) + done, take);
+        to += take;
+        len -= take;
+        done = 0;
+        idx++;
+    }
+}
+
+void sg_scatter(struct bio_vec* bv, const struct bvec_iter& it, const uint8_t* from, uint32_t len) {
+    uint32_t idx = it.bi_idx, done = it.bi_bvec_done;
+    while (len) {
+        uint32_t take = std::min(bv[idx].bv_len - done, len);
+        std::memcpy(const_cast<uint8_t*>(bv_data(bv[idx])) + done, from, take);
+        from += take;
+        len -= take;
+        done = 0;
+        idx++;
+    }
+}
+
+// Kernel bvec_iter_advance semantics: clamp (and warn) past the end.
+void iter_advance(const struct bio_vec* bv, struct bvec_iter* it, uint32_t bytes) {
+    if (bytes > it->bi_size) {
+        it->bi_size = 0;
+        return;
+    }
+    uint32_t idx = it->bi_idx;
+    it->bi_size -= bytes;
+    bytes += it->bi_bvec_done;
+    while (bytes && bytes >= bv[idx].bv_len) {
+        bytes -= bv[idx].bv_len;
+        idx++;
+    }
+    it->bi_idx = idx;
+    it->bi_bvec_done = bytes;
+}
+
+int table_type_of(const struct bio_vec* bv, const struct bvec_iter* it) {
+    // lz4e/lz4e_compress.c:184-211 (LZ4E_fillBvIterSize)
+    uint32_t size = it->bi_size, idx = it->bi_idx, done = it->bi_bvec_done, i = 0;
+    int tt = LZ4E_TABLE_BYU16;
+    while (size) {
+        const uint32_t len = bv[idx].bv_len;
+        if (i >= BIO_MAX_VECS) return 0;
+        if (i >= 16 || len > 4096) tt |= LZ4E_TABLE_BYU32;
+        if (len > (1u << 24)) tt |= LZ4E_TABLE_BYU64;
+        size -= std::min(len - done, size);
+        done = 0;
+        idx++;
+        i++;
+    }
+    return tt;
+}
+
+// Metadata block layout for a batch of R blocks (device + pinned host):
+struct MetaLayout {
+    size_t src_off, src_len, ttype, dst_off, dst_cap, ret, aux, total;
+    explicit MetaLayout(uint32_t R) {
+        size_t o = 0;
+        src_off = o; o += align16(8ull * R);
+        src_len = o; o += align16(4ull * R);
+        ttype = o;   o += align16(1ull * R);
+        dst_off = o; o += align16(8ull * R);
+        dst_cap = o; o += align16(4ull * R);
+        ret = o;     o += align16(4ull * R);
+        aux = o;     o += align16(8ull * R);
+        total = o;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* lz4e_last_error(void) { return g_err.c_str(); }
+
+int lz4e_gpu_available(void) {
+    Ctx& c = ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    return c.init() ? 1 : 0;
+}
+
+int lz4e_sg_table_type(const struct bio_vec* src, const struct bvec_iter* it) {
+    return table_type_of(src, it);
+}
+
+int lz4e_compress_sg_batch(struct lz4e_sg_request* reqs, int n) {
+    if (n <= 0) return 0;
+    Ctx& c = ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    g_err.clear();
+    if (!c.init()) return -1;
+
+    const uint32_t R = (uint32_t)n;
+    std::vector<uint64_t> src_off(R), dst_off(R);
+    std::vector<uint32_t> src_len(R), dst_cap(R), dst_slot(R);
+    std::vector<uint8_t> ttype(R), live(R);
+    uint64_t so = 0, dso = 0;
+    uint32_t max_len = 0;
+    for (uint32_t i = 0; i < R; ++i) {
+        lz4e_sg_request& q = reqs[i];
+        q.ret = 0;
+        const uint32_t len = q.srcIter->bi_size;
+        int tt = LZ4E_TABLE_BYU16;
+        live[i] = 0;
+        if (len > LZ4E_MAX_INPUT_SIZE) continue;                                   // :245-248
+        if (len >= 13 && (tt = table_type_of(q.src, q.srcIter)) == 0) continue;    // :274-277
+        live[i] = 1;
+        src_len[i] = len;
+        ttype[i] = (uint8_t)tt;
+        dst_cap[i] = q.dstIter->bi_size;
+        dst_slot[i] = std::min(dst_cap[i], bound_of(len)) + 64;
+        src_off[i] = so;
+        so += align16(len);
+        dst_off[i] = dso;
+        dso += align16(dst_slot[i]);
+        max_len = std::max(max_len, len);
+    }
+    // Compact to the live requests.
+    std::vector<uint32_t> map;
+    for (uint32_t i = 0; i < R; ++i)
+        if (live[i]) map.push_back(i);
+    const uint32_t L = (uint32_t)map.size();
+    if (L == 0) return 0;
+    MetaLayout ml2(L);
+    const size_t data_bytes = so + dso;
+    if (!c.h_data.ensure(data_bytes) || !c.d_data.ensure(data_bytes) ||
+        !c.h_meta.ensure(ml2.total) || !c.d_meta.ensure(ml2.total))
+        return -1;
+    uint8_t* hd = static_cast<uint8_t*>(c.h_data.p);
+    uint8_t* hm = static_cast<uint8_t*>(c.h_meta.p);
+    for (uint32_t j = 0; j < L; ++j) {
+        const uint32_t i = map[j];
+        sg_gather(reqs[i].src, *reqs[i].srcIter, hd + src_off[i], src_len[i]);
+        reinterpret_cast<uint64_t*>(hm + ml2.src_off)[j] = src_off[i];
+        reinterpret_cast<uint32_t*>(hm + ml2.src_len)[j] = src_len[i];
+        (hm + ml2.ttype)[j] = ttype[i];
+        reinterpret_cast<uint64_t*>(hm + ml2.dst_off)[j] = so + dst_off[i];
+        reinterpret_cast<uint32_t*>(hm + ml2.dst_cap)[j] = dst_cap[i];
+    }
+    uint8_t* dd = static_cast<uint8_t*>(c.d_data.p);
+    uint8_t* dm = static_cast<uint8_t*>(c.d_meta.p);
+    if (!hip_ok(hipMemcpyAsync(dd, hd, so, hipMemcpyHostToDevice, c.stream), "H2D data") ||
+        !hip_ok(hipMemcpyAsync(dm, hm, ml2.ret, hipMemcpyHostToDevice, c.stream), "H2D meta"))
+        return -1;
+    lz4e::CompressBatch a{dd,
+                          reinterpret_cast<const uint64_t*>(dm + ml2.src_off),
+                          reinterpret_cast<const uint32_t*>(dm + ml2.src_len),
+                          dm + ml2.ttype,
+                          dd,
+                          reinterpret_cast<const uint64_t*>(dm + ml2.dst_off),
+                          reinterpret_cast<const uint32_t*>(dm + ml2.dst_cap),
+                          reinterpret_cast<int32_t*>(dm + ml2.ret),
+                          reinterpret_cast<uint32_t*>(dm + ml2.aux),
+                          L,
+                          max_len};
+    if (!hip_ok(lz4e::launch_compress(a, c.stream), "compress launch")) return -1;
+    if (!hip_ok(hipMemcpyAsync(hm + ml2.ret, dm + ml2.ret, ml2.total - ml2.ret,
+                               hipMemcpyDeviceToHost, c.stream), "D2H meta") ||
+        !hip_ok(hipMemcpyAsync(hd + so, dd + so, dso, hipMemcpyDeviceToHost, c.stream), "D2H data") ||
+        !hip_ok(hipStreamSynchronize(c.stream), "compress sync"))
+        return -1;
+    int ok = 0;
+    for (uint32_t j = 0; j < L; ++j) {
+        const uint32_t i = map[j];
+        lz4e_sg_request& q = reqs[i];
+        const int32_t r = reinterpret_cast<const int32_t*>(hm + ml2.ret)[j];
+        const uint32_t* aux = reinterpret_cast<const uint32_t*>(hm + ml2.aux) + 2 * j;
+        if (r <= 0) {
+            q.ret = 0;
+            continue;
+        }
+        sg_scatter(q.dst, *q.dstIter, hd + so + dst_off[i], (uint32_t)r);
+        iter_advance(q.src, q.srcIter, aux[0]);
+        iter_advance(q.dst, q.dstIter, (uint32_t)r - aux[1]);
+        q.ret = r;
+        ok++;
+    }
+    return ok;
+}
+
+int LZ4E_compress_default(const struct bio_vec* src, struct bio_vec* dst, struct bvec_iter* srcIter,
+                          struct bvec_iter* dstIter, void* wrkmem) {
+    if (wrkmem) std::memset(wrkmem, 0, LZ4E_MEM_COMPRESS);  // lz4e_compress.c:548
+    if (srcIter->bi_size > LZ4E_MAX_INPUT_SIZE) return 0;
+    lz4e_sg_request q{src, dst, srcIter, dstIter, 0};
+    const int r = lz4e_compress_sg_batch(&q, 1);
+    return r < 0 ? 0 : q.ret;
+}
+
+int lz4e_decompress_batch(const char* const* src, const int* csize, char* const* dst, const int* cap,
+                          int* ret, int n) {
+    if (n <= 0) return 0;
+    Ctx& c = ctx();
+    std::lock_guard<std::mutex> lk(c.mu);
+    g_err.clear();
+    if (!c.init()) {
+        for (int i = 0; i < n; ++i) ret[i] = -1;
+        return -1;
+    }
+    const uint32_t R = (uint32_t)n;
+    std::vector<uint64_t> so(R), dso(R);
+    uint64_t s = 0, d = 0;
+    for (uint32_t i = 0; i < R; ++i) {
+        so[i] = s;
+        s += align16((uint64_t)std::max(csize[i], 0));
+    }
+    for (uint32_t i = 0; i < R; ++i) {
+        dso[i] = s + d;
+        d += align16((uint64_t)std::max(cap[i], 0) + 64);
+    }
+    const size_t meta = align16(8ull * R) * 2 + align16(4ull * R) * 3;
+    if (!c.h_data.ensure(s + d) || !c.d_data.ensure(s + d) || !c.h_meta.ensure(meta) ||
+        !c.d_meta.ensure(meta)) {
+        for (int i = 0; i < n; ++i) ret[i] = -1;
+        return -1;
+    }
+    uint8_t* hd = static_cast<uint8_t*>(c.h_data.p);
+    uint8_t* hm = static_cast<uint8_t*>(c.h_meta.p);
+    const size_t m_so = 0, m_sl = align16(8ull * R), m_do = m_sl + align16(4ull * R),
+                 m_dc = m_do + align16(8ull * R), m_rt = m_dc + align16(4ull * R);
+    for (uint32_t i = 0; i < R; ++i) {
+        if (csize[i] > 0) std::memcpy(hd + so[i], src[i], (size_t)csize[i]);
+        reinterpret_cast<uint64_t*>(hm + m_so)[i] = so[i];
+        reinterpret_cast<int32_t*>(hm + m_sl)[i] = csize[i];
+        reinterpret_cast<uint64_t*>(hm + m_do)[i] = dso[i];
+        reinterpret_cast<int32_t*>(hm + m_dc)[i] = cap[i];
+    }
+    uint8_t* dd = static_cast<uint8_t*>(c.d_data.p);
+    uint8_t* dm = static_cast<uint8_t*>(c.d_meta.p);
+    bool ok = hip_ok(hipMemcpyAsync(dd, hd, s, hipMemcpyHostToDevice, c.stream), "H2D data") &&
+              hip_ok(hipMemcpyAsync(dm, hm, m_rt, hipMemcpyHostToDevice, c.stream), "H2D meta");
+    if (ok) {
+        lz4e::DecompressBatch a{dd,
+                                reinterpret_cast<const uint64_t*>(dm + m_so),
+                                reinterpret_cast<const int32_t*>(dm + m_sl),
+                                dd,
+                                reinterpret_cast<const uint64_t*>(dm + m_do),
+                                reinterpret_cast<const int32_t*>(dm + m_dc),
+                                reinterpret_cast<int32_t*>(dm + m_rt),
+                                R};
+        ok = hip_ok(lz4e::launch_decompress(a, c.stream), "decompress launch") &&
+             hip_ok(hipMemcpyAsync(hm + m_rt, dm + m_rt, 4ull * R, hipMemcpyDeviceToHost, c.stream),
+                    "D2H ret") &&
+             hip_ok(hipMemcpyAsync(hd + s, dd + s, d, hipMemcpyDeviceToHost, c.stream), "D2H data") &&
+             hip_ok(hipStreamSynchronize(c.stream), "decompress sync");
+    }
+    if (!ok) {
+        for (int i = 0; i < n; ++i) ret[i] = -1;
+        return -1;
+    }
+    int good = 0;
+    for (uint32_t i = 0; i < R; ++i) {
+        ret[i] = reinterpret_cast<const int32_t*>(hm + m_rt)[i];
+        if (ret[i] >= 0) {
+            if (ret[i] > 0) std::memcpy(dst[i], hd + dso[i], (size_t)ret[i]);
+            good++;
+        }
+    }
+    return good;
+}
+
+int LZ4E_decompress_safe(const char* source, char* dest, int compressedSize, int maxDecompressedSize) {
+    int r = -1;
+    char* d = dest;
+    if (lz4e_decompress_batch(&source, &compressedSize, &d, &maxDecompressedSize, &r, 1) < 0)
+        return r < 0 ? r : -1;
+    return r;
+}
+
+int lz4e_compress_batch_dev(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
+                            const uint8_t* table_type, uint8_t* dst, const uint64_t* dst_off,
+                            const uint32_t* dst_cap, int32_t* ret, uint32_t* aux, uint32_t nblocks,
+                            uint32_t max_len, void* stream) {
+    g_err.clear();
+    lz4e::CompressBatch a{src, src_off, src_len, table_type, dst, dst_off, dst_cap, ret, aux,
+                          nblocks, max_len};
+    return hip_ok(lz4e::launch_compress(a, static_cast<hipStream_t>(stream)), "compress launch") ? 0
+                                                                                                  : -1;
+}
+
+int lz4e_decompress_batch_dev(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
+                              uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
+                              int32_t* ret, uint32_t nblocks, void* stream) {
+    g_err.clear();
+    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks};
+    return hip_ok(lz4e::launch_decompress(a, static_cast<hipStream_t>(stream)), "decompress launch")
+               ? 0
+               : -1;
+}
+
+}  // extern "C"

@@ -1,0 +1,324 @@
+"""GPU parity tests: the HIP path, called through the C ABI, against the CPU
+oracle on the same seeded inputs.  Integer/byte work, so the bar is
+bit-exact: identical return values, identical frame bytes, identical
+iterator post-state, identical decoder error codes."""
+import ctypes
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ref
+from lz4e_amd import BYU16, BYU32, BYU64, compress_bound, corpus, make_sg
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+KAT = json.load(open(os.path.join(GOLDEN, "reference_kat.json")))
+
+
+def _corpus(kind, n, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "text":
+        return corpus.text_proxy(n, seed)
+    if kind == "runs":
+        return corpus._runs(n, rng)
+    if kind == "random":
+        return rng.integers(0, 256, n, dtype=np.uint8)
+    if kind == "ints":
+        return corpus._int_table(n, rng)
+    if kind == "fio":
+        return corpus.fio_pattern(n, seed)
+    if kind == "small_alpha":
+        return rng.integers(0, 3, n, dtype=np.uint8)
+    return corpus.silesia_proxy(n, seed)
+
+
+# ---------------------------------------------------------------------------
+# device batch helpers
+# ---------------------------------------------------------------------------
+
+def _gpu_compress(amd, blocks, ttypes, caps=None):
+    import torch
+    n = len(blocks)
+    lens = np.array([len(b) for b in blocks], dtype=np.int64)
+    offs = np.zeros(n, dtype=np.int64)
+    offs[1:] = np.cumsum((lens + 15) // 16 * 16)[:-1]
+    total = int(offs[-1] + lens[-1]) + 16 if n else 16
+    host = np.zeros(total, dtype=np.uint8)
+    for i, b in enumerate(blocks):
+        host[offs[i]:offs[i] + lens[i]] = np.frombuffer(bytes(b), dtype=np.uint8)
+    bounds = lens + lens // 255 + 16
+    caps = bounds if caps is None else np.asarray(caps, dtype=np.int64)
+    slot = np.minimum(caps, bounds) + 64
+    doffs = np.zeros(n, dtype=np.int64)
+    doffs[1:] = np.cumsum((slot + 15) // 16 * 16)[:-1]
+    dev = torch.device("cuda")
+    src = torch.from_numpy(host).to(dev)
+    dst = torch.zeros(int(doffs[-1] + slot[-1]) + 16, dtype=torch.uint8, device=dev)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).to(dev)
+    ret = torch.full((n,), -7, dtype=torch.int32, device=dev)
+    aux = torch.zeros(2 * n, dtype=torch.int32, device=dev)
+    amd.compress_batch_dev(src, t(offs, np.int64), t(lens, np.int32), t(ttypes, np.uint8), dst,
+                           t(doffs, np.int64), t(caps, np.int32), ret, aux)
+    torch.cuda.synchronize()
+    r = ret.cpu().numpy()
+    d = dst.cpu().numpy()
+    ax = aux.cpu().numpy().reshape(-1, 2)
+    frames = [d[doffs[i]:doffs[i] + max(r[i], 0)].tobytes() for i in range(n)]
+    return r, frames, ax
+
+
+def _gpu_decompress(amd, frames, caps, csizes=None):
+    import torch
+    n = len(frames)
+    csizes = [len(f) for f in frames] if csizes is None else csizes
+    flen = np.array([len(f) for f in frames], dtype=np.int64)
+    offs = np.zeros(n, dtype=np.int64)
+    offs[1:] = np.cumsum((flen + 15) // 16 * 16 + 16)[:-1]
+    host = np.zeros(int(offs[-1] + flen[-1]) + 16 if n else 16, dtype=np.uint8)
+    for i, f in enumerate(frames):
+        host[offs[i]:offs[i] + flen[i]] = np.frombuffer(bytes(f), dtype=np.uint8)
+    caps = np.asarray(caps, dtype=np.int64)
+    slot = np.maximum(caps, 0) + 64
+    doffs = np.zeros(n, dtype=np.int64)
+    doffs[1:] = np.cumsum((slot + 15) // 16 * 16)[:-1]
+    dev = torch.device("cuda")
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).to(dev)
+    src = torch.from_numpy(host).to(dev)
+    dst = torch.zeros(int(doffs[-1] + slot[-1]) + 16, dtype=torch.uint8, device=dev)
+    ret = torch.full((n,), -7777, dtype=torch.int32, device=dev)
+    amd.decompress_batch_dev(src, t(offs, np.int64), t(csizes, np.int32), dst, t(doffs, np.int64),
+                             t(caps, np.int32), ret)
+    torch.cuda.synchronize()
+    r = ret.cpu().numpy()
+    d = dst.cpu().numpy()
+    return r, [d[doffs[i]:doffs[i] + max(r[i], 0)].tobytes() for i in range(n)]
+
+
+# ---------------------------------------------------------------------------
+# reference known answers through the drop-in entry points
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("case", KAT["compress"], ids=lambda c: f'{c["file"]}-{len(c["segments"])}x')
+def test_kat_frames_via_compress_default(gpu, case, test_files):
+    data = test_files[case["file"]][case["start"]:case["start"] + case["len"]]
+    cap = compress_bound(len(data))
+    src = make_sg(data, case["segments"], shuffle_seed=1)
+    dst = make_sg(b"", [4096] * (-(-cap // 4096)), capacity=cap, shuffle_seed=2)
+    r = gpu.compress_default(src, dst)
+    assert r == case["size"], gpu.last_error()
+    assert hashlib.sha256(dst.read_prefix(r)).hexdigest() == case["sha256"]
+    # iterator post-state identical to the oracle's
+    src2 = make_sg(data, case["segments"], shuffle_seed=1)
+    dst2 = make_sg(b"", [4096] * (-(-cap // 4096)), capacity=cap, shuffle_seed=2)
+    assert oracle_ref.compress_sg(src2, dst2) == r
+    assert src.it.as_tuple() == src2.it.as_tuple()
+    assert dst.it.as_tuple() == dst2.it.as_tuple()
+
+
+def test_kat_decompress_codes(gpu, test_files):
+    d = KAT["decompress"]
+    data = test_files[d["frame"]["file"]][:d["frame"]["len"]]
+    frame = oracle_ref.compress(data, d["frame"]["table_type"])[1]
+    for c in d["cases"]:
+        ret, out = gpu.decompress_safe(frame[:c["csize"]], c["cap"], compressed_size=c["csize"])
+        assert ret == c["ret"], c["what"]
+        if ret > 0:
+            assert out == data
+    for c in d["single_zero_byte"]:
+        assert gpu.decompress_safe(b"\x00", c["cap"])[0] == c["ret"]
+
+
+def test_edge_cases_compress_default(gpu):
+    for n in list(range(0, 20)) + [255, 256, 4095, 4096, 4097]:
+        data = _corpus("small_alpha", n, n).tobytes()
+        src = make_sg(data, [n] if n else [1], capacity=n)
+        cap = compress_bound(n)
+        dst = make_sg(b"", [cap + 8], capacity=cap)
+        r = gpu.compress_default(src, dst)
+        assert (r, dst.read_prefix(r)) == oracle_ref.compress(data, BYU16)[:2], n
+    # 256 segments OK, 257 -> 0 (lz4e_compress.c:197-198, :274-277)
+    data = _corpus("small_alpha", 16 * 257, 3).tobytes()
+    cap = compress_bound(len(data))
+    ok = make_sg(data[:16 * 256], [16] * 256)
+    r = gpu.compress_default(ok, make_sg(b"", [cap], capacity=cap))
+    assert r == oracle_ref.compress(data[:16 * 256], BYU32)[0]
+    bad = make_sg(data, [16] * 257)
+    assert gpu.compress_default(bad, make_sg(b"", [cap], capacity=cap)) == 0
+    assert bad.it.bi_size == len(data)
+
+
+# ---------------------------------------------------------------------------
+# randomized batches against the oracle
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("kind", ["mixed", "text", "runs", "random", "ints", "fio", "small_alpha"])
+@pytest.mark.parametrize("cls", [BYU16, BYU32])
+def test_compress_batch_vs_oracle(gpu, kind, cls):
+    rng = np.random.default_rng(hash((kind, cls)) & 0xFFFF)
+    data = _corpus(kind, 1 << 21, 17)
+    lens = [int(x) for x in rng.choice([0, 1, 12, 13, 14, 100, 4096, 4097, 30000, 65535, 65536], size=48)]
+    if cls == BYU32:
+        lens += [65537, 131072, 200000]
+    blocks, starts = [], []
+    for ln in lens:
+        s = int(rng.integers(0, data.size - ln))
+        blocks.append(data[s:s + ln].tobytes())
+    ttypes = [cls] * len(blocks)
+    r, frames, aux = _gpu_compress(gpu, blocks, ttypes)
+    for i, b in enumerate(blocks):
+        er, ef, efs, elr = oracle_ref.compress(b, cls)
+        assert r[i] == er, (i, len(b))
+        assert frames[i] == ef, (i, len(b))
+        assert (aux[i][0], aux[i][1]) == (efs, elr), (i, len(b))
+
+
+def test_compress_byu64(gpu):
+    """byU64 class (a > 16 MiB segment): HBM-resident path, 2048-entry table."""
+    n = (1 << 24) + 40000
+    data = _corpus("mixed", n, 5).tobytes()
+    r, frames, _ = _gpu_compress(gpu, [data], [BYU64])
+    er, ef, _, _ = oracle_ref.compress(data, BYU64)
+    assert r[0] == er
+    assert frames[0] == ef
+
+
+@pytest.mark.parametrize("kind", ["text", "mixed", "random"])
+def test_compress_limited_output(gpu, kind):
+    """Capacities below LZ4E_COMPRESSBOUND take the limitedOutput checks."""
+    data = _corpus(kind, 1 << 20, 23)
+    rng = np.random.default_rng(7)
+    blocks, caps, ttypes = [], [], []
+    for i in range(40):
+        ln = int(rng.choice([4096, 20000, 65536]))
+        s = int(rng.integers(0, data.size - ln))
+        b = data[s:s + ln].tobytes()
+        full = oracle_ref.compress(b, BYU16)[0]
+        cap = int(max(0, full + rng.integers(-40, 12)))
+        blocks.append(b)
+        caps.append(min(cap, compress_bound(ln)))
+        ttypes.append(BYU16)
+    r, frames, _ = _gpu_compress(gpu, blocks, ttypes, caps)
+    for i, b in enumerate(blocks):
+        er, ef, _, _ = oracle_ref.compress(b, BYU16, cap=caps[i])
+        assert r[i] == er, (i, caps[i])
+        assert frames[i] == ef
+
+
+def test_compress_sg_batch_layouts(gpu):
+    rng = np.random.default_rng(99)
+    data = _corpus("mixed", 1 << 20, 31).tobytes()
+    pairs, twins = [], []
+    for i in range(24):
+        n = int(rng.integers(13, 60000))
+        s = int(rng.integers(0, len(data) - n))
+        blk = data[s:s + n]
+        if i % 2:
+            segs = [min(4096, n - k) for k in range(0, n, 4096)]
+        else:
+            segs = [min(512, n - k) for k in range(0, n, 512)]
+        offs = [int(rng.integers(0, 4096)) for _ in segs]
+        cap = compress_bound(n)
+        mk = lambda seed: (make_sg(blk, segs, offsets=offs, shuffle_seed=seed),
+                           make_sg(b"", [1000] * (-(-cap // 1000)), capacity=cap, shuffle_seed=seed))
+        pairs.append(mk(i))
+        twins.append(mk(i))
+    rets = gpu.compress_sg_batch(pairs)
+    for (s, d), (s2, d2), r in zip(pairs, twins, rets):
+        er = oracle_ref.compress_sg(s2, d2)
+        assert r == er
+        assert d.read_prefix(r) == d2.read_prefix(er)
+        assert s.it.as_tuple() == s2.it.as_tuple()
+        assert d.it.as_tuple() == d2.it.as_tuple()
+
+
+# ---------------------------------------------------------------------------
+# decoder parity (values and error codes)
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("kind", ["mixed", "text", "runs", "random", "fio", "small_alpha"])
+def test_decompress_batch_vs_oracle(gpu, kind):
+    rng = np.random.default_rng(len(kind))
+    data = _corpus(kind, 1 << 21, 41)
+    frames, caps, expect = [], [], []
+    for i in range(40):
+        ln = int(rng.choice([1, 13, 100, 4096, 65536, 200000]))
+        s = int(rng.integers(0, data.size - ln))
+        b = data[s:s + ln].tobytes()
+        f = oracle_ref.compress(b, BYU32 if ln > 65536 else BYU16)[1]
+        frames.append(f)
+        caps.append(ln + int(rng.choice([0, 0, 1, 100])))
+        expect.append(b)
+    r, outs = _gpu_decompress(gpu, frames, caps)
+    for i in range(len(frames)):
+        er, eo = oracle_ref.decompress(frames[i], caps[i])
+        assert r[i] == er == len(expect[i])
+        assert outs[i] == eo == expect[i]
+
+
+@pytest.mark.parametrize("mode", ["truncate", "flip", "garbage", "small_cap", "csize"])
+def test_decompress_error_codes(gpu, mode):
+    rng = np.random.default_rng(1234 + len(mode))
+    data = _corpus("mixed", 1 << 20, 77)
+    frames, caps, csizes = [], [], []
+    for i in range(160):
+        ln = int(rng.choice([50, 4096, 30000, 65536]))
+        s = int(rng.integers(0, data.size - ln))
+        f = bytearray(oracle_ref.compress(data[s:s + ln].tobytes(), BYU16)[1])
+        cap, cs = ln, len(f)
+        if mode == "truncate":
+            cs = int(rng.integers(0, len(f)))
+        elif mode == "flip":
+            for _ in range(int(rng.integers(1, 4))):
+                j = int(rng.integers(0, len(f)))
+                f[j] ^= 1 << int(rng.integers(0, 8))
+        elif mode == "garbage":
+            f = bytearray(rng.integers(0, 256, int(rng.integers(1, 3000)), dtype=np.uint8).tobytes())
+            cs = len(f)
+        elif mode == "small_cap":
+            cap = int(rng.integers(0, ln))
+        else:
+            cs = len(f) + int(rng.integers(-3, 0))
+        frames.append(bytes(f))
+        caps.append(cap)
+        csizes.append(cs)
+    r, outs = _gpu_decompress(gpu, frames, caps, csizes)
+    for i in range(len(frames)):
+        er, eo = oracle_ref.decompress(frames[i], caps[i], csize=csizes[i])
+        assert r[i] == er, (i, mode, caps[i], csizes[i])
+        if er >= 0:
+            assert outs[i] == eo
+
+
+def test_decompress_single_calls(gpu, test_files):
+    for name in ("01.txt", "02.txt", "03.jpg"):
+        data = test_files[name][:65536]
+        f = oracle_ref.compress(data, BYU16)[1]
+        assert gpu.decompress_safe(f, len(data)) == (len(data), data)
+        res = gpu.decompress_batch([f, f[:-1], b""], [len(data), len(data), 10])
+        assert res[0] == (len(data), data)
+        assert res[1][0] == oracle_ref.decompress(f[:-1], len(data))[0]
+        assert res[2][0] == -1
+
+
+# ---------------------------------------------------------------------------
+# full-size property: GPU round trip of the benchmark workload shape
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("cls,bs,kind", [(BYU16, 65536, "mixed"), (BYU16, 4096, "fio"),
+                                         (BYU32, 65536, "mixed"), (BYU32, 262144, "text")])
+def test_full_size_roundtrip(gpu, cls, bs, kind):
+    n_blocks = {65536: 256, 4096: 2048, 262144: 32}[bs]
+    data = _corpus(kind, n_blocks * bs, 2024)
+    blocks = [data[i * bs:(i + 1) * bs].tobytes() for i in range(n_blocks)]
+    r, frames, _ = _gpu_compress(gpu, blocks, [cls] * n_blocks)
+    assert (r > 0).all()
+    dr, outs = _gpu_decompress(gpu, frames, [bs] * n_blocks)
+    assert (dr == bs).all()
+    assert all(o == b for o, b in zip(outs, blocks))
+    # the oracle on every 8th block: identical frames
+    for i in range(0, n_blocks, 8):
+        assert frames[i] == oracle_ref.compress(blocks[i], cls)[1]
