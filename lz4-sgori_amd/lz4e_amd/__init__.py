@@ -88,6 +88,14 @@ def lib() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} missing: build it with `make -C lz4-sgori_amd` "
                           "(or __graft_entry__.build())")
+    # One HIP runtime per process: torch wheels bundle their own
+    # libamdhip64.so.7 (same soname as /opt/rocm's).  Whichever loads first is
+    # shared by both, and torch only initialises on its own copy, so when
+    # torch is installed it is imported before the library is loaded.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P, U32, I32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
     L.LZ4E_compress_default.argtypes = [ctypes.POINTER(BioVec), ctypes.POINTER(BioVec),

@@ -4,6 +4,7 @@ bit-exact: identical return values, identical frame bytes, identical
 iterator post-state, identical decoder error codes."""
 import ctypes
 import hashlib
+import zlib
 import json
 import os
 
@@ -138,8 +139,9 @@ def test_edge_cases_compress_default(gpu):
         src = make_sg(data, [n] if n else [1], capacity=n)
         cap = compress_bound(n)
         dst = make_sg(b"", [cap + 8], capacity=cap)
+        cls = oracle_ref.table_type(src) if n >= 13 else BYU16
         r = gpu.compress_default(src, dst)
-        assert (r, dst.read_prefix(r)) == oracle_ref.compress(data, BYU16)[:2], n
+        assert (r, dst.read_prefix(r)) == oracle_ref.compress(data, cls)[:2], n
     # 256 segments OK, 257 -> 0 (lz4e_compress.c:197-198, :274-277)
     data = _corpus("small_alpha", 16 * 257, 3).tobytes()
     cap = compress_bound(len(data))
@@ -158,7 +160,7 @@ def test_edge_cases_compress_default(gpu):
 @pytest.mark.parametrize("kind", ["mixed", "text", "runs", "random", "ints", "fio", "small_alpha"])
 @pytest.mark.parametrize("cls", [BYU16, BYU32])
 def test_compress_batch_vs_oracle(gpu, kind, cls):
-    rng = np.random.default_rng(hash((kind, cls)) & 0xFFFF)
+    rng = np.random.default_rng(zlib.crc32(f"{kind}-{cls}".encode()))
     data = _corpus(kind, 1 << 21, 17)
     lens = [int(x) for x in rng.choice([0, 1, 12, 13, 14, 100, 4096, 4097, 30000, 65535, 65536], size=48)]
     if cls == BYU32:
