@@ -27,14 +27,23 @@ LZ4E_DEV uint32_t lane_val(uint32_t v, uint32_t l) { return __builtin_amdgcn_rea
 LZ4E_DEV uint32_t ctz64(uint64_t m) { return (uint32_t)__builtin_ctzll(m); }
 LZ4E_DEV uint32_t popc64(uint64_t m) { return (uint32_t)__builtin_popcountll(m); }
 
+// Global-memory pointer types: pointers rebuilt from integer addresses lose
+// their address space and would otherwise compile to flat_* accesses, which
+// also count on lgkmcnt (coupling them to every LDS wait).
+typedef __attribute__((address_space(1))) const uint32_t gcu32;
+typedef __attribute__((address_space(1))) const uint8_t gcu8;
+
 // Bytes [4*i, 4*i+4) of a word image (an LDS copy of a block, or the block
 // in HBM), little endian.  The word index is clamped so that a masked-off
 // lane never reads outside the image.
-struct ClampedWords {
-    const uint32_t* w;
+template <class P>
+struct ClampedWordsT {
+    P w;
     uint32_t last;  // last readable word index
     LZ4E_DEV uint32_t word(uint32_t i) const { return w[i < last ? i : last]; }
 };
+using ClampedWords = ClampedWordsT<const uint32_t*>;  // LDS image
+using GlobalWords = ClampedWordsT<gcu32*>;            // HBM image
 
 // The byte image is addressed with a constant byte shift so that an HBM
 // block need not start on a word boundary (shift is 0 for LDS).

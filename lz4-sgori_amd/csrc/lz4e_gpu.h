@@ -38,6 +38,9 @@ struct DecompressBatch {
 
 uint32_t compress_lds_bytes(uint32_t max_len, bool lds_input);
 hipError_t launch_compress(const CompressBatch& a, hipStream_t stream);
+// Diagnostic build: per-block phase cycle counters (8 x u64 per block) into dbg.
+hipError_t launch_compress_stamped(const CompressBatch& a, hipStream_t stream, uint64_t* dbg);
 hipError_t launch_decompress(const DecompressBatch& a, hipStream_t stream);
+hipError_t launch_decompress_stamped(const DecompressBatch& a, hipStream_t stream, uint64_t* dbg);
 
 }  // namespace lz4e

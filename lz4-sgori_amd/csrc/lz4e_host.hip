@@ -410,6 +410,32 @@ int lz4e_compress_batch_dev(const uint8_t* src, const uint64_t* src_off, const u
                                                                                                   : -1;
 }
 
+// Diagnostic (not part of include/lz4e.h): the compress kernel with per-block
+// phase cycle counters, 8 x u64 per block into dbg.
+int lz4e_debug_compress_stamped(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
+                                const uint8_t* table_type, uint8_t* dst, const uint64_t* dst_off,
+                                const uint32_t* dst_cap, int32_t* ret, uint32_t nblocks,
+                                uint32_t max_len, void* stream, uint64_t* dbg) {
+    lz4e::CompressBatch a{src, src_off, src_len, table_type, dst, dst_off, dst_cap, ret, nullptr,
+                          nblocks, max_len};
+    return hip_ok(lz4e::launch_compress_stamped(a, static_cast<hipStream_t>(stream), dbg),
+                  "compress launch")
+               ? 0
+               : -1;
+}
+
+// Diagnostic (not part of include/lz4e.h): the decompress kernel with
+// per-block phase cycle counters, 8 x u64 per block into dbg.
+int lz4e_debug_decompress_stamped(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
+                                  uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
+                                  int32_t* ret, uint32_t nblocks, void* stream, uint64_t* dbg) {
+    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks};
+    return hip_ok(lz4e::launch_decompress_stamped(a, static_cast<hipStream_t>(stream), dbg),
+                  "decompress launch")
+               ? 0
+               : -1;
+}
+
 int lz4e_decompress_batch_dev(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
                               uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
                               int32_t* ret, uint32_t nblocks, void* stream) {

@@ -39,7 +39,7 @@ LZ4E_MEM_COMPRESS = 17440
 LZ4E_MAX_INPUT_SIZE = 0x7E000000
 BYU16, BYU32, BYU64 = 1, 3, 7
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblz4e_amd.so")
+LIB_PATH = os.environ.get("LZ4E_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "liblz4e_amd.so")
 
 # Every function include/lz4e.h declares.
 EXPORTED_SYMBOLS = (
