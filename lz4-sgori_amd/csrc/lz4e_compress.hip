@@ -3,33 +3,39 @@
 // Bit-exact restatement of the reference greedy parse
 // (/root/reference/lz4e/lz4e_compress.c:218-534, LZ4E_compress_generic with
 // noDict, acceleration 1), one wave64 per block, all control flow
-// wave-uniform (the parse state lives in SGPRs):
+// wave-uniform (the parse state lives in SGPRs).  The parse is a serial
+// chain of dependent round trips, so the kernel is built for the fewest
+// instructions and round trips per sequence:
 //
 //  * The hash table (8192 x u16 for byU16, 4096 x u32 for byU32, 2048 x u32
-//    for byU64) lives in LDS.  The input block is read either from an LDS
-//    copy (small blocks) or straight from HBM through L1/L2 (the 16 KiB of
-//    LDS per block then allows 10 blocks per CU).
+//    for byU64) lives in LDS (16 KiB per block).  The input block is read
+//    straight from HBM with unaligned dword loads (L1/L2 absorb the reuse),
+//    or from an LDS copy for small blocks.
 //  * Data moves in "stripes": one dword per lane, lane k holding the 4 bytes
-//    at X - 4 + 4k for a base position X.  A step loads the stripe at the
-//    current position and the stripe at its match candidate together; lane 0
-//    serves the backward catch-up (lz4e_compress.c:339-349), lane 1 the
-//    4-byte verify, lanes 2.. LZ4E_count (lz4e_defs.h:587-636) by XOR +
-//    ballot, 248 bytes per round trip.  Literal runs are stored straight from
-//    the stripe lanes; the post-match hashes (lz4e_compress.c:461-470) are
-//    read out of the stripe with v_readlane.
-//  * The dominant path on compressible data is "match, then the next
-//    position matches again" (lz4e_compress.c:486-493): one LDS round trip
-//    for the table, one data round trip for the candidate stripe.
+//    at X - 4 + 4k for a base position X.  A match step loads the stripe at
+//    the current position and at its candidate together; lane 0 serves the
+//    backward catch-up (lz4e_compress.c:339-349), XOR + ballot counts up to
+//    252 bytes per round trip (LZ4E_count, lz4e_defs.h:587-636) and, on the
+//    post-match rematch (lz4e_compress.c:461-493), the same count is the
+//    4-byte verify.  Literal runs are stored as one dword per lane straight
+//    from the stripe; the post-match hashes are read out of the stripe with
+//    v_readlane.  Token, offset and a one-byte match-length extension leave
+//    as one dword store.
 //  * Match search (lz4e_compress.c:292-336) is speculative over a window of
 //    probes, one per lane: probe positions are a closed-form function of the
 //    search start (skip step +1 every 64 probes), hashes are pure functions
 //    of the data, and the candidate a probe sees is "the latest earlier probe
 //    of the window with an equal hash, else the table entry from before the
 //    window".  Every probe writes its position and reads it back: a lane that
-//    does not see its own position shares its hash with another lane (those
-//    sets are then resolved exactly, one ballot per hash bit).  The first
+//    does not see its own position shares its hash with another lane, and
+//    those lane groups are resolved with one ballot per group.  The first
 //    verifying lane is the reference's match; the table is then fixed up to
 //    hold exactly the puts of the probes up to it.
+//
+// Stores may write up to 3 bytes past the bytes they own when a later store
+// of the same wave (program order) rewrites those bytes, and never past the
+// end of the frame: every match is followed by at least the last-literals
+// token and 5 literals.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -44,34 +50,73 @@ namespace {
 constexpr uint32_t kTableBytes = 16384;  // 1 << LZ4E_MEMORY_USAGE
 constexpr uint32_t kStripe = 256;        // bytes covered by one stripe (lane k: X-4+4k)
 
-// byU16 class: u16 positions (block <= 64 KiB); byU32/byU64: u32 positions.
-// The table lives in LDS (kG = false) or in a per-block HBM scratch slot
-// (kG = true), which frees LDS for more resident blocks per CU.
+typedef __attribute__((address_space(1))) uint8_t gu8;
 typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) uint16_t gu16;
+typedef __attribute__((address_space(1))) const uint64_t gcu64;
 
-template <int TT, bool kG>
+// byU16 class: u16 positions (block <= 64 KiB); byU32/byU64: u32 positions.
+template <int TT>
 struct Table {
     uint32_t* lds;
-    gu32* glob;
     LZ4E_DEV uint32_t get(uint32_t h) const {
-        if constexpr (kG) {
-            if constexpr (TT == kByU16) return ((gu16*)glob)[h];
-            else return glob[h];
-        } else {
-            if constexpr (TT == kByU16) return reinterpret_cast<uint16_t*>(lds)[h];
-            else return lds[h];
-        }
+        if constexpr (TT == kByU16) return reinterpret_cast<uint16_t*>(lds)[h];
+        else return lds[h];
     }
     LZ4E_DEV void put(uint32_t h, uint32_t v) const {
-        if constexpr (kG) {
-            if constexpr (TT == kByU16) ((gu16*)glob)[h] = (uint16_t)v;
-            else glob[h] = v;
-        } else {
-            if constexpr (TT == kByU16) reinterpret_cast<uint16_t*>(lds)[h] = (uint16_t)v;
-            else lds[h] = v;
-        }
+        if constexpr (TT == kByU16) reinterpret_cast<uint16_t*>(lds)[h] = (uint16_t)v;
+        else lds[h] = v;
     }
+    // Read back after a put of the whole wave: which lane's write landed is
+    // only known to the LDS, so the compiler must not forward the put.
+    LZ4E_DEV uint32_t reread(uint32_t h) const {
+        typedef __attribute__((address_space(3))) volatile uint16_t lvu16;
+        typedef __attribute__((address_space(3))) volatile uint32_t lvu32;
+        if constexpr (TT == kByU16) return ((lvu16*)lds)[h];
+        else return ((lvu32*)lds)[h];
+    }
+};
+
+// Moves a (possibly wave-uniform) byte offset into a VGPR.  A uniform load
+// from read-only memory would otherwise become s_load_*, which ignores the
+// low two address bits -- wrong for the unaligned reads below.
+LZ4E_DEV uint32_t vaddr(uint32_t q) {
+    asm("" : "+v"(q));
+    return q;
+}
+
+// A block in HBM, read with unaligned vector loads (gfx950 global loads need
+// no alignment).  n >= kMinLength whenever the parse runs.
+struct HbmImage {
+    gcu8* p;
+    uint32_t n;
+    LZ4E_DEV uint32_t rd8(uint32_t q) const { return p[q]; }
+    LZ4E_DEV uint32_t ld32(uint32_t q) const { return *(gcu32*)(p + vaddr(q)); }
+    LZ4E_DEV uint64_t ld64(uint32_t q) const { return *(gcu64*)(p + vaddr(q)); }
+    // Lanes past the block (or before it, X < 4) read a clamped, meaningless
+    // dword; every consumer masks those bytes.
+    LZ4E_DEV uint32_t stripe(uint32_t X, uint32_t lane) const {
+        const uint32_t q = X - 4 + 4 * lane;
+        return ld32(q < n - 4 ? q : n - 4);
+    }
+};
+
+// A block staged in LDS as words (the last partial word zero-padded).
+struct LdsImage {
+    const uint32_t* w;
+    uint32_t last;  // last word index
+    LZ4E_DEV uint32_t word(uint32_t i) const { return w[i < last ? i : last]; }
+    LZ4E_DEV uint32_t rd8(uint32_t q) const { return (word(q >> 2) >> ((q & 3) * 8)) & 0xFFu; }
+    LZ4E_DEV uint32_t ld32(uint32_t q) const {
+        const uint32_t i = q >> 2;
+        return __builtin_amdgcn_alignbyte(word(i + 1), word(i), q & 3);
+    }
+    LZ4E_DEV uint64_t ld64(uint32_t q) const {
+        const uint32_t i = q >> 2, r = q & 3;
+        const uint32_t w0 = word(i), w1 = word(i + 1), w2 = word(i + 2);
+        return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, r) << 32) |
+               __builtin_amdgcn_alignbyte(w1, w0, r);
+    }
+    LZ4E_DEV uint32_t stripe(uint32_t X, uint32_t lane) const { return ld32(X - 4 + 4 * lane); }
 };
 
 // Phase cycle counters of the diagnostic build (launch_compress_stamped).
@@ -91,38 +136,35 @@ struct Stamps {
 };
 enum { kPhSearch, kPhStripe, kPhLit, kPhCount, kPhRematch, kPhTail };
 
-// ---- stripe helpers ---------------------------------------------------------
+// Event trace of the stamped build when compiled with -DLZ4E_TRACE (debug
+// only): (kind << 56 | a, b) pairs after the 8 stamp words of the block.
+#ifdef LZ4E_TRACE
+#define LZ4E_TR(k, a, b)                                                              \
+    do {                                                                              \
+        if (kStamps && dbg && lane == 0 && trn < (1u << 16)) {                        \
+            dbg[8 + 2 * trn] = ((uint64_t)(k) << 56) | (uint64_t)(a);                 \
+            dbg[9 + 2 * trn] = (uint64_t)(b);                                         \
+        }                                                                             \
+        trn++;                                                                        \
+    } while (0)
+#else
+#define LZ4E_TR(k, a, b) \
+    do {                 \
+    } while (0)
+#endif
 
-// 4 bytes at byte index u of a stripe (u + 4 <= 256), wave-uniform result.
-LZ4E_DEV uint32_t stripe_u32(uint32_t sv, uint32_t u) {
-    const uint32_t k = u >> 2, r = u & 3;
-    const uint32_t lo = lane_val(sv, k);
-    if (r == 0) return lo;
-    const uint32_t hi = lane_val(sv, k + 1);
-    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * r));
+// hash of the position whose bytes are v (hash5 for byU32, hash4 otherwise;
+// hashLog 13 / 12 / 11 for byU16 / byU32 / byU64, lz4e_compress.c:48-96)
+template <int TT>
+LZ4E_DEV uint32_t hash_val(uint64_t v) {
+    if constexpr (TT == kByU32) return hash5(v, 12);
+    else return hash4((uint32_t)v, TT == kByU16 ? 13 : 11);
 }
 
-// 8 bytes at byte index u (u + 8 <= 256); only the low 40 bits matter to hash5.
-LZ4E_DEV uint64_t stripe_u64(uint32_t sv, uint32_t u) {
-    const uint32_t lo = stripe_u32(sv, u), hi = stripe_u32(sv, u + 4);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-template <class IMG>
-LZ4E_DEV uint32_t stripe_load(const IMG& img, uint32_t X, uint32_t lane) {
-    // Lane 0 of a stripe based below position 4 reaches before the block:
-    // those byte slots read as zero (the catch-up never looks at them).
-    const int32_t p = (int32_t)(X + 4 * lane) - 4;
-    const uint32_t v = img.rd32(p < 0 ? 0u : (uint32_t)p);
-    return p < 0 ? (p <= -4 ? 0u : v << (8 * (uint32_t)(-p))) : v;
-}
-
-// First byte index u >= u0 where the two stripes differ, or where the
-// comparison limit u0 + lim is reached; kStripe if neither happens.
-LZ4E_DEV uint32_t stripe_mismatch(uint32_t x, uint32_t u0, uint32_t lim, uint32_t lane) {
+// First byte index u >= u0 where the two stripes differ (x = si ^ sb), or
+// where the comparison limit e is reached; kStripe if neither happens.
+LZ4E_DEV uint32_t stripe_mismatch(uint32_t x, uint32_t u0, uint32_t e, uint32_t lane) {
     const uint32_t b = 4 * lane;
-    const uint64_t e64 = (uint64_t)u0 + lim;
-    const uint32_t e = e64 > kStripe ? kStripe + 4 : (uint32_t)e64;
     if (b + 4 <= u0) x = 0;
     else if (b < u0) x &= ~0u << (8 * (u0 - b));
     if (b >= e) x |= 1u;
@@ -133,17 +175,11 @@ LZ4E_DEV uint32_t stripe_mismatch(uint32_t x, uint32_t u0, uint32_t lim, uint32_
     return 4 * f + (uint32_t)__builtin_ctz(lane_val(x, f)) / 8;
 }
 
-// hash of the position whose bytes are v (hash5 for byU32, hash4 otherwise;
-// hashLog 13 / 12 / 11 for byU16 / byU32 / byU64, lz4e_compress.c:48-96)
-template <int TT>
-LZ4E_DEV uint32_t hash_val(uint64_t v) {
-    if constexpr (TT == kByU32) return hash5(v, 12);
-    else return hash4((uint32_t)v, TT == kByU16 ? 13 : 11);
-}
-
 // ---- output -------------------------------------------------------------
 
-LZ4E_DEV uint32_t out_ext(uint8_t* out, uint32_t at, uint32_t rest, uint32_t lane) {
+LZ4E_DEV void st32(gu8* out, uint32_t at, uint32_t v) { *(gu32*)(out + at) = v; }
+
+LZ4E_DEV uint32_t out_ext(gu8* out, uint32_t at, uint32_t rest, uint32_t lane) {
     // (rest)/255 bytes of 0xFF then rest % 255 (lz4e_compress.c:365-377, :432-447)
     const uint32_t nff = rest / 255;
     for (uint32_t k = lane; k < nff; k += kWave) out[at + k] = 0xFF;
@@ -151,56 +187,56 @@ LZ4E_DEV uint32_t out_ext(uint8_t* out, uint32_t at, uint32_t rest, uint32_t lan
     return nff + 1;
 }
 
-// Literal copy from the image: 4 bytes per lane, 4 words in flight per lane.
+// Literal copy of len bytes from the image, whole dwords (may write 3 bytes
+// past len; from + len + 3 must stay inside the block).
 template <class IMG>
-LZ4E_DEV void out_copy(uint8_t* out, uint32_t at, const IMG& img, uint32_t from, uint32_t len,
+LZ4E_DEV void out_copy(gu8* out, uint32_t at, const IMG& img, uint32_t from, uint32_t len,
                        uint32_t lane) {
     constexpr uint32_t kChunk = 4 * 4 * kWave;
     for (uint32_t base = 0; base < len; base += kChunk) {
         uint32_t w[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) w[j] = img.rd32(from + base + 4 * (j * kWave + lane));
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = base + 4 * (j * kWave + lane);
+            w[j] = k < len ? img.ld32(from + k) : 0;
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t k = base + 4 * (j * kWave + lane);
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                if (k + b < len) out[at + k + b] = (uint8_t)(w[j] >> (8 * b));
+            if (k < len) st32(out, at + k, w[j]);
         }
     }
 }
 
-// Literal bytes [from, from+len) taken from the stripe based at X (they must
-// lie inside it): every lane stores its own bytes, 4 masked byte stores.
-LZ4E_DEV void out_copy_stripe(uint8_t* out, uint32_t at, uint32_t sv, uint32_t X, uint32_t from,
-                              uint32_t len, uint32_t lane) {
-    const int32_t rel = (int32_t)(X - 4 + 4 * lane) - (int32_t)from;  // offset of this lane's byte 0
-#pragma unroll
-    for (int b = 0; b < 4; ++b) {
-        const int32_t t = rel + b;
-        if (t >= 0 && t < (int32_t)len) out[at + t] = (uint8_t)(sv >> (8 * b));
-    }
+// Exact copy of the last literals (nothing may be written past the frame).
+template <class IMG>
+LZ4E_DEV void out_copy_exact(gu8* out, uint32_t at, const IMG& img, uint32_t from, uint32_t len,
+                             uint32_t lane) {
+    const uint32_t whole = len & ~3u;
+    out_copy(out, at, img, from, whole, lane);
+    if (lane < len - whole) out[at + whole + lane] = (uint8_t)img.rd8(from + whole + lane);
 }
 
-template <int TT, bool kStamps, bool kG, class IMG>
-LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, gu32* gtab, uint32_t n, uint8_t* out,
-                             uint32_t cap, int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg,
-                             uint32_t lane) {
-    constexpr uint32_t hlog = TT == kByU64 ? 11 : (TT == kByU32 ? 12 : 13);
-    const Table<TT, kG> T{smem, gtab};
+template <int TT, bool kStamps, class IMG>
+LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* out, uint32_t cap,
+                             int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg, uint32_t lane) {
+    const Table<TT> T{smem};
     const uint64_t bound = (uint64_t)n + n / 255 + 16;
     const bool limited = cap < bound;  // lz4e_compress.c:553-560
     uint32_t op = 0, anchor = 0, ip = 0;
+    [[maybe_unused]] uint32_t trn = 0;
     Stamps st;
     if (kStamps) st.start();
 
     if (n >= kMinLength) {
         const uint32_t mflimit = n - kMfLimit;
         const uint32_t matchlimit = n - kLastLiterals;
-        // Front stripe: based at the anchor of the coming search.  put(0) of
-        // the first byte stores position 0 == an empty slot, so nothing to do.
+        const uint64_t lanes_below = (1ull << lane) - 1;
+        // Front stripe: based at the anchor A of the coming search (A is
+        // always the anchor).  put(0) of the first byte stores position 0 ==
+        // an empty slot, so nothing to do.
         uint32_t A = 0;
-        uint32_t sa = stripe_load(img, A, lane);
+        uint32_t sa = img.stripe(A, lane);
         uint32_t s = 1;  // search start
         for (;;) {
             uint32_t cand;
@@ -209,55 +245,58 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, gu32* gtab, uint32_
                 uint32_t pbase = 0;
                 for (;;) {
                     const uint32_t P = pbase + lane;
-                    const uint64_t q64 = (uint64_t)s + probe_offset(P);
-                    const bool valid = q64 + probe_step(P) <= mflimit;
+                    const uint32_t qq = s + (uint32_t)probe_offset(P);
+                    const bool valid = (uint64_t)qq + probe_step(P) <= mflimit;
                     const uint64_t vmask = ballot(valid);
                     if (vmask == 0) {
-                        if (pbase != 0) ip = s + (uint32_t)probe_offset(pbase - 1);
-                        else ip = s;
+                        ip = pbase != 0 ? s + (uint32_t)probe_offset(pbase - 1) : s;
                         if (kStamps) st.lap(kPhSearch);
                         goto last_literals;
                     }
-                    const uint32_t q = valid ? (uint32_t)q64 : s;
+                    const uint32_t q = valid ? qq : s;
                     uint64_t v;
-                    if (pbase == 0 && s + 64 + 8 <= A - 4 + kStripe) {
+                    if (s + (uint32_t)probe_offset(pbase + kWave - 1) + 8 <= A - 4 + kStripe) {
                         // probe bytes from the front stripe (ds_bpermute, no memory)
                         const uint32_t t = q - (A - 4);
                         const uint32_t j = t >> 2, r = t & 3;
-                        const uint32_t w0 = __shfl(sa, j), w1 = __shfl(sa, j + 1),
-                                       w2 = __shfl(sa, j + 2);
-                        v = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, r) << 32) |
-                            __builtin_amdgcn_alignbyte(w1, w0, r);
+                        const uint32_t w0 = __shfl(sa, j), w1 = __shfl(sa, j + 1);
+                        // hash5 reads 5 bytes: byte t+4 is byte r of w1 (the
+                        // bytes above it do not enter the hash)
+                        uint32_t hi = 0;
+                        if constexpr (TT == kByU32) hi = __builtin_amdgcn_alignbyte(w1, w1, r);
+                        v = ((uint64_t)hi << 32) | __builtin_amdgcn_alignbyte(w1, w0, r);
+                    } else if constexpr (TT == kByU32) {
+                        v = img.ld64(q);
                     } else {
-                        v = img.rd64(q);
+                        v = img.ld32(q);
                     }
                     const uint32_t vq = (uint32_t)v;
-                    const uint32_t h = valid ? hash_val<TT>(v) : 0;
-                    uint32_t c0 = 0;
+                    const uint32_t h = hash_val<TT>(v);
+                    uint32_t c0 = 0, rb = q;
                     if (valid) {
                         c0 = T.get(h);  // table entry from before this window
                         T.put(h, q);    // speculative put of every probe
+                        rb = T.reread(h);
                     }
-                    const uint64_t cm = ballot(valid && T.get(h) != q);
-                    uint64_t same = 1ull << lane;
+                    const uint64_t cm = ballot(rb != q);
+                    uint64_t same = 0;  // valid lanes sharing my hash (clash groups only)
                     uint32_t c = c0;
                     if (cm) {
-                        // Exact equal-hash lane sets, one ballot per hash bit.
-                        same = vmask;
-                        for (uint32_t bit = 0; bit < hlog; ++bit) {
-                            const bool hb = (h >> bit) & 1;
-                            const uint64_t m = ballot(valid && hb);
-                            same &= hb ? m : ~m;
-                        }
-                        const uint64_t below = same & ((1ull << lane) - 1);
-                        const uint32_t pl = below ? 63 - (uint32_t)__builtin_clzll(below) : lane;
-                        const uint32_t qp = __shfl(q, pl);
+                        uint64_t todo = cm;
+                        do {
+                            const uint32_t hg = lane_val(h, ctz64(todo));
+                            const uint64_t m = ballot(valid && h == hg);
+                            if (h == hg) same = m;
+                            todo &= ~m;
+                        } while (todo);
+                        const uint64_t below = same & lanes_below;
+                        const uint32_t qp = __shfl(q, below ? 63 - (uint32_t)__builtin_clzll(below) : lane);
                         if (below) c = qp;  // latest earlier probe, same hash
                     }
                     bool hit = false;
                     if (valid) {
                         const bool dist_ok = (TT == kByU16) || (c + kMaxDistance >= q);
-                        hit = dist_ok && img.rd32(c) == vq;
+                        hit = dist_ok && img.ld32(c) == vq;
                     }
                     const uint64_t hm = ballot(hit);
                     const uint32_t klast = hm ? ctz64(hm) : popc64(vmask) - 1;
@@ -277,6 +316,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, gu32* gtab, uint32_
                     if (hm) {
                         ip = lane_val(q, klast);
                         cand = lane_val(c, klast);
+                        LZ4E_TR(1, ip, ((uint64_t)pbase << 32) | cand);
                         if (kStamps) { st.cnt[0]++; st.lap(kPhSearch); }
                         break;
                     }
@@ -290,30 +330,33 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, gu32* gtab, uint32_
             }
 
             // ================= stripes at (ip, cand), catch-up ==============
-            uint32_t X = ip, Y = cand;  // stripe bases
-            uint32_t si = stripe_load(img, X, lane);
-            uint32_t sb = stripe_load(img, Y, lane);
+            uint32_t X = ip;  // base of si; sb is based at cand + (X - ip)
+            uint32_t si = img.stripe(ip, lane);
+            uint32_t sb = img.stripe(cand, lane);
             {
                 uint32_t room = ip - anchor < cand ? ip - anchor : cand;
                 if (room) {
-                    // lane 0 holds the 4 bytes before ip / before cand
-                    const uint32_t x = lane_val(si, 0) ^ lane_val(sb, 0);
-                    uint32_t c = x ? (uint32_t)__builtin_clz(x) / 8 : 4;
-                    if (c > room) c = room;
+                    uint32_t c = 0;
+                    if (cand >= 4) {
+                        // lane 0 holds the 4 bytes before ip / before cand
+                        const uint32_t x = lane_val(si, 0) ^ lane_val(sb, 0);
+                        c = x ? (uint32_t)__builtin_clz(x) / 8 : 4;
+                        if (c > room) c = room;
+                    }
                     ip -= c;
                     cand -= c;
                     room -= c;
-                    if (c == 4 && room) {
-                        // long catch-up (rare): byte steps from memory
+                    if (room && (c == 4 || cand + c < 4)) {
+                        // long catch-up or a candidate near the block start
+                        // (rare): byte steps, then fresh stripes
                         while (room && img.rd8(ip - 1) == img.rd8(cand - 1)) {
                             ip--;
                             cand--;
                             room--;
                         }
                         X = ip;
-                        Y = cand;
-                        si = stripe_load(img, X, lane);
-                        sb = stripe_load(img, Y, lane);
+                        si = img.stripe(ip, lane);
+                        sb = img.stripe(cand, lane);
                     }
                 }
             }
@@ -331,88 +374,138 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, gu32* gtab, uint32_
                 } else {
                     token = L << 4;
                 }
-                if (anchor >= A - 4 && ip <= A - 4 + kStripe)
-                    out_copy_stripe(out, op, sa, A, anchor, L, lane);
-                else
+                if (L <= kStripe - 4) {
+                    // bytes [A, A+252) sit in lanes 1.. of the front stripe
+                    if (lane >= 1 && 4 * (lane - 1) < L) st32(out, op + 4 * (lane - 1), sa);
+                } else {
                     out_copy(out, op, img, anchor, L, lane);
+                }
                 op += L;
             }
             if (kStamps) st.lap(kPhLit);
 
             // ================= match chain ===================================
+            // Each pass counts the match at ip against cand from the stripes
+            // si (base X) / sb, then tries the rematch.  A sequence's stores
+            // are issued after the loads of the next step: on gfx9 vmcnt also
+            // counts stores, so stores issued earlier would delay every
+            // following load wait by their write acknowledgement.
             for (;;) {
-                // offset (lz4e_compress.c:386-387)
-                const uint32_t off = ip - cand;
-                if (lane == 0) {
-                    out[op] = (uint8_t)off;
-                    out[op + 1] = (uint8_t)(off >> 8);
+                // LZ4E_count from ip (lz4e_compress.c:420-423, the first 4
+                // bytes are known equal): matched bytes t, mc = t - 4.
+                const uint32_t u_ip = ip + 4 - X;  // ip's byte index in the stripes
+                const uint32_t lim = matchlimit - ip;
+                uint32_t u;
+                if (u_ip + lim >= kStripe) {
+                    uint32_t x = si ^ sb;
+                    if (lane == 0) x = u_ip >= 4 ? 0u : x & (~0u << (8 * u_ip));
+                    const uint64_t mm = ballot(x != 0);
+                    u = mm ? 4 * ctz64(mm) + (uint32_t)__builtin_ctz(lane_val(x, ctz64(mm))) / 8
+                           : kStripe;
+                } else {
+                    u = stripe_mismatch(si ^ sb, u_ip, u_ip + lim, lane);
                 }
-                op += 2;
-                // LZ4E_count from ip+4 / cand+4 (lz4e_compress.c:420-423)
-                uint32_t mc = 0;
-                {
-                    const uint32_t lim = matchlimit - (ip + 4);
-                    uint32_t u0 = ip + 4 - (X - 4);  // same offset in both stripes
+                uint32_t t = u - u_ip;
+                if (u == kStripe) {
+                    // long match: fresh stripe pairs, 252 bytes per round trip
                     for (;;) {
-                        const uint32_t u = stripe_mismatch(si ^ sb, u0, lim - mc, lane);
-                        if (u < kStripe) {
-                            mc += u - u0;
-                            break;
-                        }
-                        mc += kStripe - u0;
-                        X = ip + 4 + mc;
-                        Y = cand + 4 + mc;
-                        si = stripe_load(img, X, lane);
-                        sb = stripe_load(img, Y, lane);
-                        u0 = 4;
+                        X = ip + t;
+                        si = img.stripe(ip + t, lane);
+                        sb = img.stripe(cand + t, lane);
+                        u = stripe_mismatch(si ^ sb, 4, 4 + lim - t, lane);
+                        t += u - 4;
+                        if (u < kStripe) break;
                     }
                 }
-                ip += 4 + mc;
-                if (limited && (uint64_t)op + 6 + (mc >> 8) > cap) goto fail;
-                if (mc >= 15) {
-                    token += 15;
-                    op += out_ext(out, op, mc - 15, lane);
-                } else {
-                    token += mc;
+                LZ4E_TR(2, ip, ((uint64_t)cand << 32) | t);
+                if (t < 4) {
+                    op = tok;  // rematch verify failed (lz4e_compress.c:486-493)
+                    break;
                 }
-                if (lane == 0) out[tok] = (uint8_t)token;
+                // sequence record: token (at tok), [lit ext + literals],
+                // offset (at op_off), match-length extension
+                const uint32_t mc = t - 4;
+                const uint32_t off = ip - cand;
+                const uint32_t op_off = op;
+                op += 2;
+                if (limited && (uint64_t)op + 6 + (mc >> 8) > cap) goto fail;
+                const uint32_t tokb = token | (mc < 15 ? mc : 15);
+                const uint32_t e1 = mc - 15;  // extension bytes when mc >= 15
+                if (mc >= 15) op += e1 / 255 + 1;
+                const uint32_t tok_at = tok;
+                auto emit = [&]() {
+                    const uint32_t e1w = (mc >= 15 && e1 < 255) ? e1 : 0;
+                    if (lane == 0) {
+                        if (op_off == tok_at + 1) {
+                            st32(out, tok_at, tokb | (off << 8) | (e1w << 24));
+                        } else {
+                            out[tok_at] = (uint8_t)tokb;
+                            st32(out, op_off, off | (e1w << 16));
+                        }
+                    }
+                    if (mc >= 15 && e1 >= 255) out_ext(out, op_off + 2, e1, lane);
+                };
+#ifndef LZ4E_EMIT_LATE
+                emit();
+#endif
+                ip += t;
                 anchor = ip;
                 if (kStamps) { st.cnt[1]++; st.lap(kPhCount); }
-                if (ip > mflimit) goto last_literals;  // :456-457
+                if (ip > mflimit) {  // :456-457
+#ifdef LZ4E_EMIT_LATE
+                    emit();
+#endif
+                    goto last_literals;
+                }
 
                 // ---- fill table at ip-2, test ip (lz4e_compress.c:461-493) ----
-                uint64_t v1, v2;
-                if (ip + 8 <= X - 4 + kStripe) {
-                    v1 = stripe_u64(si, ip - 2 - (X - 4));
-                    v2 = stripe_u64(si, ip - (X - 4));
+                const uint32_t sn = img.stripe(ip, lane);
+                // hash inputs ip-2 .. ip+4 read out of the current stripe, or
+                // (match ending at its top) out of the new one, which is then
+                // waited for: two branches, so the common path never waits.
+                uint32_t uu = ip - 2 - (X - 4), w0, w1, w2;
+                if (uu <= 4 * 61 + 3) {
+                    const uint32_t k = uu >> 2;
+                    w0 = lane_val(si, k);
+                    w1 = lane_val(si, k + 1);
+                    w2 = lane_val(si, k + 2);
                 } else {
-                    v1 = img.rd64(ip - 2);
-                    v2 = img.rd64(ip);
+                    asm volatile("" ::: "memory");
+                    uu = 2;  // ip-2 is byte 2 of the new stripe
+                    w0 = lane_val(sn, 0);
+                    w1 = lane_val(sn, 1);
+                    w2 = lane_val(sn, 2);
                 }
-                const uint32_t sn = stripe_load(img, ip, lane);  // overlaps the table access
+                uint64_t v1, v2;
+                {
+                    const uint32_t r = uu & 3;
+                    const uint64_t lo = ((uint64_t)w1 << 32) | w0, hi = ((uint64_t)w2 << 32) | w1;
+                    v1 = lo >> (8 * r);
+                    v2 = r < 2 ? lo >> (8 * (r + 2)) : hi >> (8 * (r - 2));
+                }
                 const uint32_t h1 = hash_val<TT>(v1);
                 const uint32_t h2 = hash_val<TT>(v2);
                 T.put(h1, ip - 2);
                 const uint32_t c2 = uni(T.get(h2));
                 T.put(h2, ip);
+                LZ4E_TR(3, ip, ((uint64_t)h2 << 32) | c2);
+                LZ4E_TR(4, ip - 2, h1);
                 X = ip;
                 si = sn;
-                if (c2 + kMaxDistance >= ip) {
-                    Y = c2;
-                    sb = stripe_load(img, Y, lane);
-                    if (lane_val(sb, 1) == lane_val(si, 1)) {
-                        cand = c2;
-                        tok = op++;
-                        token = 0;
-                        if (kStamps) { st.cnt[2]++; st.lap(kPhRematch); }
-                        continue;
-                    }
-                }
-                if (kStamps) st.lap(kPhRematch);
-                break;
+                const bool near = c2 + kMaxDistance >= ip;
+                if (near) sb = img.stripe(c2, lane);
+#ifdef LZ4E_EMIT_LATE
+                emit();
+#endif
+                if (!near) break;
+                cand = c2;
+                tok = op++;
+                token = 0;
+                if (kStamps) { st.cnt[2]++; st.lap(kPhRematch); }
             }
             // no match at ip: the next search starts at ip + 1 (:496-497) and
             // the stripe at ip becomes the front stripe
+            if (kStamps) st.lap(kPhRematch);
             A = ip;
             sa = si;
             s = ip + 1;
@@ -431,7 +524,7 @@ last_literals: {
             if (lane == 0) out[op] = (uint8_t)(R << 4);
             op += 1;
         }
-        out_copy(out, op, img, anchor, R, lane);
+        out_copy_exact(out, op, img, anchor, R, lane);
         if (lane == 0) {
             *ret_slot = (int32_t)(op + R);
             if (aux_slot) {
@@ -461,8 +554,7 @@ fail:
 
 // Stage a block into LDS as a word image, the bytes of the last partial word
 // zeroed (16-B loads when the block is 16-B aligned in HBM).  Reads past the
-// image are clamped to its last word (ClampedWords), so no pad is needed and
-// a 64 KiB block + its 16 KiB table fill exactly half of a CU's LDS.
+// image are clamped to its last word (LdsImage), so no pad is needed.
 LZ4E_DEV void stage_block(uint32_t* dstw, const uint8_t* src, uint32_t n, uint32_t lane) {
     const uint32_t padded = (n + 3) & ~3u;
     uint8_t* d8 = reinterpret_cast<uint8_t*>(dstw);
@@ -489,22 +581,19 @@ LZ4E_DEV void stage_block(uint32_t* dstw, const uint8_t* src, uint32_t n, uint32
     }
 }
 
-template <bool kStamps, bool kG, class IMG>
-LZ4E_DEV void dispatch_class(const IMG& img, uint32_t* smem, gu32* gtab, uint32_t n, int tt,
-                             uint8_t* out, uint32_t cap, int32_t* ret_slot, uint32_t* aux_slot,
-                             uint64_t* dbg, uint32_t lane) {
+template <bool kStamps, class IMG>
+LZ4E_DEV void dispatch_class(const IMG& img, uint32_t* smem, uint32_t n, int tt, gu8* out,
+                             uint32_t cap, int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg,
+                             uint32_t lane) {
     if (tt == kByU32)
-        compress_block<kByU32, kStamps, kG>(img, smem, gtab, n, out, cap, ret_slot, aux_slot, dbg,
-                                            lane);
+        compress_block<kByU32, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane);
     else if (tt == kByU16)
-        compress_block<kByU16, kStamps, kG>(img, smem, gtab, n, out, cap, ret_slot, aux_slot, dbg,
-                                            lane);
+        compress_block<kByU16, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane);
     else
-        compress_block<kByU64, kStamps, kG>(img, smem, gtab, n, out, cap, ret_slot, aux_slot, dbg,
-                                            lane);
+        compress_block<kByU64, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane);
 }
 
-template <bool kLdsInput, bool kStamps, bool kG>
+template <bool kLdsInput, bool kStamps>
 __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict__ src,
                                                       const uint64_t* __restrict__ src_off,
                                                       const uint32_t* __restrict__ src_len,
@@ -514,8 +603,7 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
                                                       const uint32_t* __restrict__ dst_cap,
                                                       int32_t* __restrict__ ret,
                                                       uint32_t* __restrict__ aux, uint32_t nblocks,
-                                                      uint64_t* __restrict__ dbg,
-                                                      uint32_t* __restrict__ gtab_all) {
+                                                      uint64_t* __restrict__ dbg) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t b = blockIdx.x;
     if (b >= nblocks) return;
@@ -523,7 +611,7 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
     const uint32_t n = src_len[b];
     const int tt = table_type[b];
     const uint32_t cap = dst_cap[b];
-    uint8_t* out = dst + dst_off[b];
+    gu8* out = (gu8*)(dst + dst_off[b]);
     const uint8_t* in = src + src_off[b];
     uint32_t* aux_slot = aux ? aux + 2 * (size_t)b : nullptr;
     uint64_t* dbg_slot = dbg ? dbg + 8 * (size_t)b : nullptr;
@@ -536,35 +624,22 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
         return;
     }
 
-    gu32* gtab = kG ? (gu32*)(gtab_all + (size_t)b * (kTableBytes / 4)) : nullptr;
     if (n >= kMinLength) {
         // memset of the state (lz4e_compress.c:548): 16 KiB of table.
-        if constexpr (kG) {
-            typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-            __attribute__((address_space(1))) v4u* t4 = (__attribute__((address_space(1))) v4u*)gtab;
-            for (uint32_t i = lane; i < kTableBytes / 16; i += kWave) t4[i] = v4u{0, 0, 0, 0};
-        } else {
-            uint4* t4 = reinterpret_cast<uint4*>(smem);
-            for (uint32_t i = lane; i < kTableBytes / 16; i += kWave) t4[i] = make_uint4(0, 0, 0, 0);
-        }
+        uint4* t4 = reinterpret_cast<uint4*>(smem);
+        for (uint32_t i = lane; i < kTableBytes / 16; i += kWave) t4[i] = make_uint4(0, 0, 0, 0);
     }
 
     if constexpr (kLdsInput) {
         uint32_t* inw = smem + kTableBytes / 4;
         stage_block(inw, in, n, lane);
         __syncthreads();
-        ByteImage<ClampedWords> img{ClampedWords{inw, n == 0 ? 0 : (n - 1) >> 2}, 0};
-        dispatch_class<kStamps, kG>(img, smem, gtab, n, tt, out, cap, ret + b, aux_slot, dbg_slot,
-                                    lane);
+        const LdsImage img{inw, n == 0 ? 0 : (n - 1) >> 2};
+        dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane);
     } else {
         __syncthreads();
-        const uintptr_t a = reinterpret_cast<uintptr_t>(in);
-        const uint32_t shift = (uint32_t)(a & 3);
-        gcu32* w = (gcu32*)(a - shift);
-        const uint32_t last = n + shift == 0 ? 0 : (n + shift - 1) >> 2;
-        ByteImage<GlobalWords> img{GlobalWords{w, last}, shift};
-        dispatch_class<kStamps, kG>(img, smem, gtab, n, tt, out, cap, ret + b, aux_slot, dbg_slot,
-                                    lane);
+        const HbmImage img{(gcu8*)in, n};
+        dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane);
     }
 }
 
@@ -573,47 +648,22 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
     return e ? (uint32_t)strtoul(e, nullptr, 10) : dflt;
 }
 
-// Per-block HBM table scratch for the global-table variant (grown on demand;
-// experiments via LZ4E_COMPRESS_GTABLE=1).
-uint32_t* gtable_scratch(uint32_t nblocks) {
-    static uint32_t* p = nullptr;
-    static size_t cap = 0;
-    const size_t need = (size_t)nblocks * kTableBytes;
-    if (need > cap) {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        if (hipMalloc(&p, need) != hipSuccess) return nullptr;
-        cap = need;
-    }
-    return p;
-}
-
 template <bool kStamps>
 hipError_t launch_compress_impl(const CompressBatch& a, hipStream_t stream, uint64_t* dbg) {
     if (a.nblocks == 0) return hipSuccess;
     // LZ4E_COMPRESS_LDS_MAX (bytes) overrides the LDS staging limit (experiments).
     static const uint32_t lds_max = env_u32("LZ4E_COMPRESS_LDS_MAX", kMaxLdsInput);
-    static const uint32_t gtable = env_u32("LZ4E_COMPRESS_GTABLE", 0);
     const bool lds_input = a.max_len <= lds_max;
     const dim3 grid(a.nblocks), block(kWave);
-    if (gtable && !lds_input) {
-        uint32_t* gt = gtable_scratch(a.nblocks);
-        if (!gt) return hipErrorOutOfMemory;
-        hipLaunchKernelGGL((compress_kernel<false, kStamps, true>), grid, block, 0, stream, a.src,
-                           a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.aux, a.nblocks, dbg, gt);
-        return hipGetLastError();
-    }
     const uint32_t lds = compress_lds_bytes(a.max_len, lds_input);
     if (lds_input) {
-        hipLaunchKernelGGL((compress_kernel<true, kStamps, false>), grid, block, lds, stream, a.src,
+        hipLaunchKernelGGL((compress_kernel<true, kStamps>), grid, block, lds, stream, a.src,
                            a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.aux, a.nblocks, dbg, nullptr);
+                           a.aux, a.nblocks, dbg);
     } else {
-        hipLaunchKernelGGL((compress_kernel<false, kStamps, false>), grid, block, lds, stream, a.src,
+        hipLaunchKernelGGL((compress_kernel<false, kStamps>), grid, block, lds, stream, a.src,
                            a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.aux, a.nblocks, dbg, nullptr);
+                           a.aux, a.nblocks, dbg);
     }
     return hipGetLastError();
 }
