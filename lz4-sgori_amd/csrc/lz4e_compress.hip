@@ -76,14 +76,6 @@ struct Table {
     }
 };
 
-// Moves a (possibly wave-uniform) byte offset into a VGPR.  A uniform load
-// from read-only memory would otherwise become s_load_*, which ignores the
-// low two address bits -- wrong for the unaligned reads below.
-LZ4E_DEV uint32_t vaddr(uint32_t q) {
-    asm("" : "+v"(q));
-    return q;
-}
-
 // A block in HBM, read with unaligned vector loads (gfx950 global loads need
 // no alignment).  n >= kMinLength whenever the parse runs.
 struct HbmImage {
@@ -108,13 +100,13 @@ struct LdsImage {
     LZ4E_DEV uint32_t rd8(uint32_t q) const { return (word(q >> 2) >> ((q & 3) * 8)) & 0xFFu; }
     LZ4E_DEV uint32_t ld32(uint32_t q) const {
         const uint32_t i = q >> 2;
-        return __builtin_amdgcn_alignbyte(word(i + 1), word(i), q & 3);
+        return alignbyte(word(i + 1), word(i), q & 3);
     }
     LZ4E_DEV uint64_t ld64(uint32_t q) const {
         const uint32_t i = q >> 2, r = q & 3;
         const uint32_t w0 = word(i), w1 = word(i + 1), w2 = word(i + 2);
-        return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, r) << 32) |
-               __builtin_amdgcn_alignbyte(w1, w0, r);
+        return ((uint64_t)alignbyte(w2, w1, r) << 32) |
+               alignbyte(w1, w0, r);
     }
     LZ4E_DEV uint32_t stripe(uint32_t X, uint32_t lane) const { return ld32(X - 4 + 4 * lane); }
 };
@@ -124,12 +116,12 @@ struct Stamps {
     uint64_t t, acc[6];
     uint32_t cnt[4];
     LZ4E_DEV void start() {
-        t = __builtin_amdgcn_s_memtime();
+        t = clock64();
         for (int i = 0; i < 6; ++i) acc[i] = 0;
         for (int i = 0; i < 4; ++i) cnt[i] = 0;
     }
     LZ4E_DEV void lap(int phase) {
-        const uint64_t now = __builtin_amdgcn_s_memtime();
+        const uint64_t now = clock64();
         acc[phase] += now - t;
         t = now;
     }
@@ -217,6 +209,85 @@ LZ4E_DEV void out_copy_exact(gu8* out, uint32_t at, const IMG& img, uint32_t fro
     if (lane < len - whole) out[at + whole + lane] = (uint8_t)img.rd8(from + whole + lane);
 }
 
+// Matched bytes from p against c (c < p), counting on from t bytes known
+// equal, at most matchlimit - p (LZ4E_count, lz4e_defs.h:587-636); with
+// t = 0 a result below 4 means the 4-byte verify failed.
+template <class IMG>
+LZ4E_DEV uint32_t count_from(const IMG& img, uint32_t p, uint32_t c, uint32_t t,
+                             uint32_t matchlimit, uint32_t lane) {
+    const uint32_t lim = matchlimit - p;
+    while (t < lim) {
+        const uint32_t si = img.stripe(p + t, lane);
+        const uint32_t sb = img.stripe(c + t, lane);
+        const uint32_t u = stripe_mismatch(si ^ sb, 4, 4 + lim - t, lane);
+        t += u - 4;
+        if (u < kStripe) break;
+    }
+    return t < lim ? t : lim;
+}
+
+// Bytes equal going backwards from p-1 / c-1, at most room (the catch-up of
+// lz4e_compress.c:339-349), a byte per step (rare paths only).
+template <class IMG>
+LZ4E_DEV uint32_t back_from(const IMG& img, uint32_t p, uint32_t c, uint32_t room) {
+    uint32_t b = 0;
+    while (b < room && img.rd8(p - 1 - b) == img.rd8(c - 1 - b)) ++b;
+    return b;
+}
+
+constexpr uint32_t kLong = 1u << 31;  // ml flag: 16 bytes equal, the count goes on
+constexpr uint32_t kNoBk = 0xFF;   // bk: backward bytes not available in registers
+
+// Forward match of the 16 bytes a[] against b[], lane-wise: 0 if the first 4
+// bytes differ, the matched length capped at lim, or 16 | kLong.
+LZ4E_DEV uint32_t fwd16(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t b0,
+                        uint32_t b1, uint32_t b2, uint32_t b3, uint32_t lim) {
+    const uint32_t x0 = a0 ^ b0, x1 = a1 ^ b1, x2 = a2 ^ b2, x3 = a3 ^ b3;
+    if (x0) return 0;
+    uint32_t m;
+    if (x1) m = 4 + ((uint32_t)__builtin_ctz(x1) >> 3);
+    else if (x2) m = 8 + ((uint32_t)__builtin_ctz(x2) >> 3);
+    else if (x3) m = 12 + ((uint32_t)__builtin_ctz(x3) >> 3);
+    else m = 16;
+    if (m >= lim) return lim;
+    return m == 16 ? (16 | kLong) : m;
+}
+
+// Equal bytes at the top of two dwords (backward catch-up, up to 4).
+LZ4E_DEV uint32_t back4(uint32_t a, uint32_t b) {
+    const uint32_t x = a ^ b;
+    return x ? (uint32_t)__builtin_clz(x) >> 3 : 4;
+}
+
+LZ4E_DEV uint64_t lane_val64(uint64_t v, uint32_t k) {
+    return ((uint64_t)lane_val((uint32_t)(v >> 32), k) << 32) | lane_val((uint32_t)v, k);
+}
+
+// Lanes a..b (inclusive), a <= b <= 63.
+LZ4E_DEV uint64_t lane_range(uint32_t a, uint32_t b) {
+    return (b >= 63 ? ~0ull : ((2ull << b) - 1)) & ~((1ull << a) - 1);
+}
+
+// The greedy parse in windows of 64 positions, lane k <-> position B + k.
+//
+// Window setup (all lanes at once): the 20 bytes around each position, its
+// hash, the table entry before the window (c0, the "snapshot"), the forward
+// match against c0 (ml, up to 16 bytes) and the bytes equal before both
+// (bk).  Positions sharing a hash inside the window form clash groups
+// (speculative put + read-back); for those the same quantities are also
+// taken against the previous group member (mlp, bkp).
+//
+// Walk (wave-uniform, mostly SALU): the reference parse over the window,
+// reading the precomputed lanes with v_readlane.  The candidate of a
+// position is the latest put of its hash made in the window before it, else
+// the snapshot -- exactly what the reference's table holds at that point
+// because the window's puts only touch the hashes of window positions.
+//  * rematch at a match end e (lz4e_compress.c:461-493): puts e-2 and e,
+//    candidate of e, a match iff ml != 0;
+//  * search (lz4e_compress.c:292-336): probes P <= 64 advance by one byte,
+//    so a search over the window is "first probe lane with a hit", every
+//    probe before it put; probes with larger steps go to the generic search.
+// The window's puts are written to the table once, when the walk leaves it.
 template <int TT, bool kStamps, class IMG>
 LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* out, uint32_t cap,
                              int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg, uint32_t lane) {
@@ -232,283 +303,384 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
         const uint32_t mflimit = n - kMfLimit;
         const uint32_t matchlimit = n - kLastLiterals;
         const uint64_t lanes_below = (1ull << lane) - 1;
-        // Front stripe: based at the anchor A of the coming search (A is
-        // always the anchor).  put(0) of the first byte stores position 0 ==
-        // an empty slot, so nothing to do.
-        uint32_t A = 0;
-        uint32_t sa = img.stripe(A, lane);
-        uint32_t s = 1;  // search start
+        auto clampq = [&](uint32_t q) { return q < n - 4 ? q : n - 4; };
+
+        // ---- sequence output -------------------------------------------
+        // offset, match-length code and token of a sequence whose token slot
+        // is tok (lz4e_compress.c:384-453); false when the output is full.
+        auto emit_match = [&](uint32_t tok, uint32_t tokhi, uint32_t off, uint32_t mc) -> bool {
+            const uint32_t op_off = op;
+            op += 2;
+            if (limited && (uint64_t)op + 6 + (mc >> 8) > cap) return false;
+            const uint32_t tokb = tokhi | (mc < 15 ? mc : 15);
+            const uint32_t e1 = mc - 15;
+            const uint32_t e1w = (mc >= 15 && e1 < 255) ? e1 : 0;
+            if (lane == 0) {
+                if (op_off == tok + 1) {
+                    st32(out, tok, tokb | (off << 8) | (e1w << 24));
+                } else {
+                    out[tok] = (uint8_t)tokb;
+                    st32(out, op_off, off | (e1w << 16));
+                }
+            }
+            if (mc >= 15) {
+                if (e1 < 255) {
+                    op += 1;
+                } else {
+                    lockstep();  // overwrites the dword's spare byte
+                    op += out_ext(out, op, e1, lane);
+                }
+            }
+            return true;
+        };
+
+        bool rmode = false;  // e is a match end (rematch) / the next probe of a search
+        uint32_t e = 1;      // next position of the walk
+        uint32_t s = 1;      // start of the current search
+        uint32_t jb = 0;     // probes of the current search done so far
         for (;;) {
-            uint32_t cand;
-            // ================= match search (lz4e_compress.c:292-336) ======
+            // ================= window setup =================================
+            const uint32_t B = rmode ? e - 2 : e;
+            const uint32_t p = B + lane;
+            const bool valid = p <= mflimit;  // every put / lookup is at <= mflimit
+            const uint32_t dm1 = img.ld32(clampq(p - 4)), d0 = img.ld32(clampq(p)),
+                           d1 = img.ld32(clampq(p + 4)), d2 = img.ld32(clampq(p + 8)),
+                           d3 = img.ld32(clampq(p + 12));
+            const uint32_t h = hash_val<TT>(((uint64_t)d1 << 32) | d0);
+            uint32_t c0 = 0, rb = p;
+            lockstep();  // the previous window's commit is in the table
+            if (valid) c0 = T.get(h);  // snapshot
+            lockstep();
+            if (valid) T.put(h, p);  // speculative put of every position
+            lockstep();
+            if (valid) rb = T.reread(h);
+            const uint64_t cm = ballot(rb != p);
+            uint64_t same = 0;  // valid lanes sharing my hash (clash groups only)
+            if (cm) {
+                uint64_t todo = cm;
+                do {
+                    const uint32_t hg = lane_val(h, ctz64(todo));
+                    const uint64_t m = ballot(valid && h == hg);
+                    if (h == hg) same = m;
+                    todo &= ~m;
+                } while (todo);
+            }
+            const uint64_t clash = ballot(same != 0);
+            const uint32_t lim = matchlimit - p;
+            uint32_t ml = 0, bk = kNoBk;
             {
-                uint32_t pbase = 0;
-                for (;;) {
-                    const uint32_t P = pbase + lane;
-                    const uint32_t qq = s + (uint32_t)probe_offset(P);
-                    const bool valid = (uint64_t)qq + probe_step(P) <= mflimit;
-                    const uint64_t vmask = ballot(valid);
-                    if (vmask == 0) {
-                        ip = pbase != 0 ? s + (uint32_t)probe_offset(pbase - 1) : s;
-                        if (kStamps) st.lap(kPhSearch);
-                        goto last_literals;
-                    }
-                    const uint32_t q = valid ? qq : s;
-                    uint64_t v;
-                    if (s + (uint32_t)probe_offset(pbase + kWave - 1) + 8 <= A - 4 + kStripe) {
-                        // probe bytes from the front stripe (ds_bpermute, no memory)
-                        const uint32_t t = q - (A - 4);
-                        const uint32_t j = t >> 2, r = t & 3;
-                        const uint32_t w0 = __shfl(sa, j), w1 = __shfl(sa, j + 1);
-                        // hash5 reads 5 bytes: byte t+4 is byte r of w1 (the
-                        // bytes above it do not enter the hash)
-                        uint32_t hi = 0;
-                        if constexpr (TT == kByU32) hi = __builtin_amdgcn_alignbyte(w1, w1, r);
-                        v = ((uint64_t)hi << 32) | __builtin_amdgcn_alignbyte(w1, w0, r);
-                    } else if constexpr (TT == kByU32) {
-                        v = img.ld64(q);
-                    } else {
-                        v = img.ld32(q);
-                    }
-                    const uint32_t vq = (uint32_t)v;
-                    const uint32_t h = hash_val<TT>(v);
-                    uint32_t c0 = 0, rb = q;
-                    if (valid) {
-                        c0 = T.get(h);  // table entry from before this window
-                        T.put(h, q);    // speculative put of every probe
-                        rb = T.reread(h);
-                    }
-                    const uint64_t cm = ballot(rb != q);
-                    uint64_t same = 0;  // valid lanes sharing my hash (clash groups only)
-                    uint32_t c = c0;
-                    if (cm) {
-                        uint64_t todo = cm;
-                        do {
-                            const uint32_t hg = lane_val(h, ctz64(todo));
-                            const uint64_t m = ballot(valid && h == hg);
-                            if (h == hg) same = m;
-                            todo &= ~m;
-                        } while (todo);
-                        const uint64_t below = same & lanes_below;
-                        const uint32_t qp = __shfl(q, below ? 63 - (uint32_t)__builtin_clzll(below) : lane);
-                        if (below) c = qp;  // latest earlier probe, same hash
-                    }
-                    bool hit = false;
-                    if (valid) {
-                        const bool dist_ok = (TT == kByU16) || (c + kMaxDistance >= q);
-                        hit = dist_ok && img.ld32(c) == vq;
-                    }
-                    const uint64_t hm = ballot(hit);
-                    const uint32_t klast = hm ? ctz64(hm) : popc64(vmask) - 1;
-                    // Make the table hold exactly the puts of probes 0..klast.
-                    if (valid) {
-                        if (cm == 0) {
-                            if (lane > klast) T.put(h, c0);
+                const uint32_t em1 = img.ld32(clampq(c0 - 4)), e0 = img.ld32(c0),
+                               e1 = img.ld32(clampq(c0 + 4)), e2 = img.ld32(clampq(c0 + 8)),
+                               e3 = img.ld32(clampq(c0 + 12));
+                const bool dist_ok = (TT == kByU16) || (c0 + kMaxDistance >= p);
+                if (valid && dist_ok) ml = fwd16(d0, d1, d2, d3, e0, e1, e2, e3, lim);
+                if (p >= 4 && c0 >= 4) bk = back4(dm1, em1);
+            }
+            uint32_t pl = kNoBk, mlp = 0, bkp = kNoBk;
+            if (clash) {
+                // against the previous member of the group (bytes via ds_bpermute)
+                const uint64_t below = same & lanes_below;
+                const uint32_t src = below ? 63 - (uint32_t)__builtin_clzll(below) : lane;
+                const uint32_t fm1 = shfl(dm1, src), f0 = shfl(d0, src), f1 = shfl(d1, src),
+                               f2 = shfl(d2, src), f3 = shfl(d3, src);
+                if (below) {
+                    pl = src;
+                    if (valid) mlp = fwd16(d0, d1, d2, d3, f0, f1, f2, f3, lim);
+                    if (p >= 4 && B + src >= 4) bkp = back4(dm1, fm1);
+                }
+            }
+            const uint64_t hitm = ballot(ml != 0);
+            uint64_t put = 0;
+            bool generic = false;
+            if (kStamps) { st.cnt[0]++; st.lap(kPhSearch); }
+
+            // ================= walk =========================================
+            for (;;) {
+                if (rmode) {
+                    // ---- fill table at e-2, test e (lz4e_compress.c:461-493) ----
+                    const uint32_t k = e - B;
+                    if (k > 63) break;
+                    const uint64_t prior = put | (1ull << (k - 2));
+                    uint32_t c, m;
+                    if ((clash >> k) & 1) {
+                        const uint64_t pm = lane_val64(same, k) & prior & ((1ull << k) - 1);
+                        if (pm == 0) {
+                            c = lane_val(c0, k);
+                            m = lane_val(ml, k);
                         } else {
-                            const uint64_t upto = klast >= 63 ? ~0ull : ((2ull << klast) - 1);
-                            if (lane <= klast) {
-                                if ((same & upto & ~((2ull << lane) - 1)) == 0) T.put(h, q);
-                            } else if ((same & upto) == 0) {
-                                T.put(h, c0);
+                            const uint32_t cl = 63 - (uint32_t)__builtin_clzll(pm);
+                            c = B + cl;
+                            if (cl == lane_val(pl, k)) {
+                                m = lane_val(mlp, k);
+                            } else {
+                                m = count_from(img, e, c, 0, matchlimit, lane);
+                                if (m < 4) m = 0;
+                                if (kStamps) st.cnt[2]++;
                             }
                         }
+                    } else {
+                        c = lane_val(c0, k);
+                        m = lane_val(ml, k);
                     }
-                    if (hm) {
-                        ip = lane_val(q, klast);
-                        cand = lane_val(c, klast);
-                        LZ4E_TR(1, ip, ((uint64_t)pbase << 32) | cand);
-                        if (kStamps) { st.cnt[0]++; st.lap(kPhSearch); }
-                        break;
+                    put = prior | (1ull << k);
+                    if (m == 0) {
+                        // no match at e: search from e + 1 (:496-497)
+                        rmode = false;
+                        s = e = e + 1;
+                        jb = 0;
+                        continue;
                     }
-                    if (vmask != ~0ull) {
-                        ip = lane_val(q, klast);  // last probe that ran
-                        if (kStamps) st.lap(kPhSearch);
+                    uint32_t t = m & ~kLong;
+                    if (m & kLong) t = count_from(img, e, c, 16, matchlimit, lane);
+                    LZ4E_TR(2, e, ((uint64_t)c << 32) | t);
+                    const uint32_t tok = op++;
+                    if (!emit_match(tok, 0, e - c, t - 4)) goto fail;
+                    if (kStamps) st.cnt[1]++;
+                    e += t;
+                    anchor = e;
+                    if (e > mflimit) {  // :456-457
+                        ip = e;
                         goto last_literals;
                     }
-                    pbase += kWave;
+                    continue;
                 }
-            }
 
-            // ================= stripes at (ip, cand), catch-up ==============
-            uint32_t X = ip;  // base of si; sb is based at cand + (X - ip)
-            uint32_t si = img.stripe(ip, lane);
-            uint32_t sb = img.stripe(cand, lane);
-            {
-                uint32_t room = ip - anchor < cand ? ip - anchor : cand;
-                if (room) {
-                    uint32_t c = 0;
-                    if (cand >= 4) {
-                        // lane 0 holds the 4 bytes before ip / before cand
-                        const uint32_t x = lane_val(si, 0) ^ lane_val(sb, 0);
-                        c = x ? (uint32_t)__builtin_clz(x) / 8 : 4;
-                        if (c > room) c = room;
-                    }
-                    ip -= c;
-                    cand -= c;
-                    room -= c;
-                    if (room && (c == 4 || cand + c < 4)) {
-                        // long catch-up or a candidate near the block start
-                        // (rare): byte steps, then fresh stripes
-                        while (room && img.rd8(ip - 1) == img.rd8(cand - 1)) {
-                            ip--;
-                            cand--;
-                            room--;
+                // ---- search: probes P = jb + (k - k0) at lanes k >= k0 ----
+                const uint32_t k0 = e - B;
+                if (k0 > 63) break;
+                const uint32_t kmax = k0 + 64 - jb < 63 ? k0 + 64 - jb : 63;  // P <= 64: step 1
+                // probe q runs iff q + 1 <= mflimit (:301-302)
+                const int32_t lvs = (int32_t)mflimit - 1 - (int32_t)B;
+                if (lvs < (int32_t)k0) {
+                    ip = jb ? e - 1 : s;  // the last probe that ran
+                    goto last_literals;
+                }
+                const uint32_t lastv = (uint32_t)lvs < kmax ? (uint32_t)lvs : kmax;
+                const uint64_t rng = lane_range(k0, lastv);
+                const uint64_t A = hitm & ~clash & rng;
+                uint64_t CL = clash & rng;
+                if (A) CL &= (1ull << ctz64(A)) - 1;
+                uint32_t hk = 64, c = 0, m = 0, b = kNoBk;
+                while (CL) {
+                    // a clash lane before the first plain hit: its candidate
+                    // is the latest earlier put of its group, else c0
+                    const uint32_t k = ctz64(CL);
+                    CL &= CL - 1;
+                    const uint64_t prior = put | (k > k0 ? lane_range(k0, k - 1) : 0);
+                    const uint64_t pm = lane_val64(same, k) & prior & ((1ull << k) - 1);
+                    if (pm == 0) {
+                        c = lane_val(c0, k);
+                        m = lane_val(ml, k);
+                        b = lane_val(bk, k);
+                    } else {
+                        const uint32_t cl = 63 - (uint32_t)__builtin_clzll(pm);
+                        c = B + cl;
+                        if (cl == lane_val(pl, k)) {
+                            m = lane_val(mlp, k);
+                            b = lane_val(bkp, k);
+                        } else {
+                            m = count_from(img, B + k, c, 0, matchlimit, lane);
+                            if (m < 4) m = 0;
+                            b = kNoBk;
+                            if (kStamps) st.cnt[2]++;
                         }
-                        X = ip;
-                        si = img.stripe(ip, lane);
-                        sb = img.stripe(cand, lane);
+                    }
+                    if (m) {
+                        hk = k;
+                        break;
                     }
                 }
-            }
-            if (kStamps) st.lap(kPhStripe);
-
-            uint32_t tok, token;
-            // ================= literals (lz4e_compress.c:352-382) ===========
-            {
-                const uint32_t L = ip - anchor;
-                tok = op++;
+                if (hk == 64 && A) {
+                    hk = ctz64(A);
+                    c = lane_val(c0, hk);
+                    m = lane_val(ml, hk);
+                    b = lane_val(bk, hk);
+                }
+                if (hk == 64) {
+                    // no hit among this window's probes: all of them put
+                    put |= rng;
+                    jb += lastv - k0 + 1;
+                    e = B + lastv + 1;
+                    if (lastv < kmax) {  // the next probe would pass mflimit
+                        ip = B + lastv;
+                        goto last_literals;
+                    }
+                    if (jb > 64) {  // skip steps > 1 from here: generic search
+                        generic = true;
+                        break;
+                    }
+                    continue;  // next window
+                }
+                put |= lane_range(k0, hk);
+                const uint32_t q = B + hk;
+                // catch up (lz4e_compress.c:339-349)
+                const uint32_t room = q - anchor < c ? q - anchor : c;
+                uint32_t cu;
+                if (b == kNoBk) {
+                    cu = back_from(img, q, c, room);
+                } else {
+                    cu = b < room ? b : room;
+                    if (cu == 4 && room > 4) cu += back_from(img, q - 4, c - 4, room - 4);
+                }
+                const uint32_t ipm = q - cu, cand = c - cu;
+                uint32_t t = m & ~kLong;
+                if (m & kLong) t = count_from(img, q, c, 16, matchlimit, lane);
+                t += cu;
+                LZ4E_TR(2, ipm, ((uint64_t)cand << 32) | t);
+                // literals [anchor, ipm) (lz4e_compress.c:352-382)
+                const uint32_t L = ipm - anchor;
+                const uint32_t tok = op++;
                 if (limited && (uint64_t)op + L + 8 + L / 255 > cap) goto fail;
+                uint32_t tokhi;
                 if (L >= 15) {
-                    token = 0xF0;
+                    tokhi = 0xF0;
                     op += out_ext(out, op, L - 15, lane);
                 } else {
-                    token = L << 4;
+                    tokhi = L << 4;
                 }
-                if (L <= kStripe - 4) {
-                    // bytes [A, A+252) sit in lanes 1.. of the front stripe
-                    if (lane >= 1 && 4 * (lane - 1) < L) st32(out, op + 4 * (lane - 1), sa);
+                if (anchor >= B) {
+                    // the run lies in the window: lane a0 + 4i stores bytes 4i..4i+3
+                    const uint32_t r = lane - (anchor - B);
+                    if ((r & 3) == 0 && r < L) st32(out, op + r, d0);
                 } else {
                     out_copy(out, op, img, anchor, L, lane);
                 }
                 op += L;
-            }
-            if (kStamps) st.lap(kPhLit);
-
-            // ================= match chain ===================================
-            // Each pass counts the match at ip against cand from the stripes
-            // si (base X) / sb, then tries the rematch.  A sequence's stores
-            // are issued after the loads of the next step: on gfx9 vmcnt also
-            // counts stores, so stores issued earlier would delay every
-            // following load wait by their write acknowledgement.
-            for (;;) {
-                // LZ4E_count from ip (lz4e_compress.c:420-423, the first 4
-                // bytes are known equal): matched bytes t, mc = t - 4.
-                const uint32_t u_ip = ip + 4 - X;  // ip's byte index in the stripes
-                const uint32_t lim = matchlimit - ip;
-                uint32_t u;
-                if (u_ip + lim >= kStripe) {
-                    uint32_t x = si ^ sb;
-                    if (lane == 0) x = u_ip >= 4 ? 0u : x & (~0u << (8 * u_ip));
-                    const uint64_t mm = ballot(x != 0);
-                    u = mm ? 4 * ctz64(mm) + (uint32_t)__builtin_ctz(lane_val(x, ctz64(mm))) / 8
-                           : kStripe;
-                } else {
-                    u = stripe_mismatch(si ^ sb, u_ip, u_ip + lim, lane);
-                }
-                uint32_t t = u - u_ip;
-                if (u == kStripe) {
-                    // long match: fresh stripe pairs, 252 bytes per round trip
-                    for (;;) {
-                        X = ip + t;
-                        si = img.stripe(ip + t, lane);
-                        sb = img.stripe(cand + t, lane);
-                        u = stripe_mismatch(si ^ sb, 4, 4 + lim - t, lane);
-                        t += u - 4;
-                        if (u < kStripe) break;
-                    }
-                }
-                LZ4E_TR(2, ip, ((uint64_t)cand << 32) | t);
-                if (t < 4) {
-                    op = tok;  // rematch verify failed (lz4e_compress.c:486-493)
-                    break;
-                }
-                // sequence record: token (at tok), [lit ext + literals],
-                // offset (at op_off), match-length extension
-                const uint32_t mc = t - 4;
-                const uint32_t off = ip - cand;
-                const uint32_t op_off = op;
-                op += 2;
-                if (limited && (uint64_t)op + 6 + (mc >> 8) > cap) goto fail;
-                const uint32_t tokb = token | (mc < 15 ? mc : 15);
-                const uint32_t e1 = mc - 15;  // extension bytes when mc >= 15
-                if (mc >= 15) op += e1 / 255 + 1;
-                const uint32_t tok_at = tok;
-                auto emit = [&]() {
-                    const uint32_t e1w = (mc >= 15 && e1 < 255) ? e1 : 0;
-                    if (lane == 0) {
-                        if (op_off == tok_at + 1) {
-                            st32(out, tok_at, tokb | (off << 8) | (e1w << 24));
-                        } else {
-                            out[tok_at] = (uint8_t)tokb;
-                            st32(out, op_off, off | (e1w << 16));
-                        }
-                    }
-                    if (mc >= 15 && e1 >= 255) out_ext(out, op_off + 2, e1, lane);
-                };
-#ifndef LZ4E_EMIT_LATE
-                emit();
-#endif
-                ip += t;
-                anchor = ip;
-                if (kStamps) { st.cnt[1]++; st.lap(kPhCount); }
-                if (ip > mflimit) {  // :456-457
-#ifdef LZ4E_EMIT_LATE
-                    emit();
-#endif
+                lockstep();  // the offset overwrites the copy's spare bytes
+                if (!emit_match(tok, tokhi, ipm - cand, t - 4)) goto fail;
+                if (kStamps) st.cnt[1]++;
+                e = ipm + t;
+                anchor = e;
+                rmode = true;
+                if (e > mflimit) {
+                    ip = e;
                     goto last_literals;
                 }
-
-                // ---- fill table at ip-2, test ip (lz4e_compress.c:461-493) ----
-                const uint32_t sn = img.stripe(ip, lane);
-                // hash inputs ip-2 .. ip+4 read out of the current stripe, or
-                // (match ending at its top) out of the new one, which is then
-                // waited for: two branches, so the common path never waits.
-                uint32_t uu = ip - 2 - (X - 4), w0, w1, w2;
-                if (uu <= 4 * 61 + 3) {
-                    const uint32_t k = uu >> 2;
-                    w0 = lane_val(si, k);
-                    w1 = lane_val(si, k + 1);
-                    w2 = lane_val(si, k + 2);
-                } else {
-                    asm volatile("" ::: "memory");
-                    uu = 2;  // ip-2 is byte 2 of the new stripe
-                    w0 = lane_val(sn, 0);
-                    w1 = lane_val(sn, 1);
-                    w2 = lane_val(sn, 2);
-                }
-                uint64_t v1, v2;
-                {
-                    const uint32_t r = uu & 3;
-                    const uint64_t lo = ((uint64_t)w1 << 32) | w0, hi = ((uint64_t)w2 << 32) | w1;
-                    v1 = lo >> (8 * r);
-                    v2 = r < 2 ? lo >> (8 * (r + 2)) : hi >> (8 * (r - 2));
-                }
-                const uint32_t h1 = hash_val<TT>(v1);
-                const uint32_t h2 = hash_val<TT>(v2);
-                T.put(h1, ip - 2);
-                const uint32_t c2 = uni(T.get(h2));
-                T.put(h2, ip);
-                LZ4E_TR(3, ip, ((uint64_t)h2 << 32) | c2);
-                LZ4E_TR(4, ip - 2, h1);
-                X = ip;
-                si = sn;
-                const bool near = c2 + kMaxDistance >= ip;
-                if (near) sb = img.stripe(c2, lane);
-#ifdef LZ4E_EMIT_LATE
-                emit();
-#endif
-                if (!near) break;
-                cand = c2;
-                tok = op++;
-                token = 0;
-                if (kStamps) { st.cnt[2]++; st.lap(kPhRematch); }
             }
-            // no match at ip: the next search starts at ip + 1 (:496-497) and
-            // the stripe at ip becomes the front stripe
+            if (kStamps) st.lap(kPhStripe);
+
+            // ================= commit the window's puts =====================
+            if (valid) {
+                const uint64_t pg = same & put;
+                bool writer;
+                uint32_t v;
+                if (same == 0) {
+                    writer = true;
+                    v = (put >> lane) & 1 ? p : c0;
+                } else if (pg) {
+                    writer = lane == 63 - (uint32_t)__builtin_clzll(pg);
+                    v = p;
+                } else {
+                    writer = lane == ctz64(same);
+                    v = c0;
+                }
+                if (writer) T.put(h, v);
+            }
             if (kStamps) st.lap(kPhRematch);
-            A = ip;
-            sa = si;
-            s = ip + 1;
+            if (!generic) continue;
+
+            // ================= generic search (probes P >= 65) ==============
+            // Skip steps > 1 (lz4e_compress.c:292-336) over windows of 64
+            // probes: the candidate a probe sees is the latest earlier probe
+            // of the window with an equal hash, else the table entry.
+            {
+                uint32_t pbase = jb, qh, ch;
+                for (;;) {
+                    const uint32_t P = pbase + lane;
+                    const uint32_t qq = s + (uint32_t)probe_offset(P);
+                    const bool pv = (uint64_t)qq + probe_step(P) <= mflimit;
+                    const uint64_t vmask = ballot(pv);
+                    if (vmask == 0) {
+                        ip = s + (uint32_t)probe_offset(pbase - 1);
+                        goto last_literals;
+                    }
+                    const uint32_t q = pv ? qq : s;
+                    uint64_t v;
+                    if constexpr (TT == kByU32) v = img.ld64(q);
+                    else v = img.ld32(q);
+                    const uint32_t vq = (uint32_t)v;
+                    const uint32_t hq = hash_val<TT>(v);
+                    uint32_t g0 = 0, grb = q;
+                    lockstep();
+                    if (pv) g0 = T.get(hq);
+                    lockstep();
+                    if (pv) T.put(hq, q);
+                    lockstep();
+                    if (pv) grb = T.reread(hq);
+                    const uint64_t gcm = ballot(grb != q);
+                    uint64_t gsame = 0;
+                    uint32_t gc = g0;
+                    if (gcm) {
+                        uint64_t todo = gcm;
+                        do {
+                            const uint32_t hg = lane_val(hq, ctz64(todo));
+                            const uint64_t mm = ballot(pv && hq == hg);
+                            if (hq == hg) gsame = mm;
+                            todo &= ~mm;
+                        } while (todo);
+                        const uint64_t below = gsame & lanes_below;
+                        const uint32_t qp =
+                            shfl(q, below ? 63 - (uint32_t)__builtin_clzll(below) : lane);
+                        if (below) gc = qp;
+                    }
+                    bool hit = false;
+                    if (pv) {
+                        const bool dist_ok = (TT == kByU16) || (gc + kMaxDistance >= q);
+                        hit = dist_ok && img.ld32(gc) == vq;
+                    }
+                    const uint64_t hm = ballot(hit);
+                    const uint32_t klast = hm ? ctz64(hm) : popc64(vmask) - 1;
+                    if (pv) {
+                        if (gcm == 0) {
+                            if (lane > klast) T.put(hq, g0);
+                        } else {
+                            const uint64_t upto = klast >= 63 ? ~0ull : ((2ull << klast) - 1);
+                            if (lane <= klast) {
+                                if ((gsame & upto & ~((2ull << lane) - 1)) == 0) T.put(hq, q);
+                            } else if ((gsame & upto) == 0) {
+                                T.put(hq, g0);
+                            }
+                        }
+                    }
+                    if (hm) {
+                        qh = lane_val(q, klast);
+                        ch = lane_val(gc, klast);
+                        break;
+                    }
+                    if (vmask != ~0ull) {
+                        ip = lane_val(q, klast);  // the last probe that ran
+                        goto last_literals;
+                    }
+                    pbase += kWave;
+                }
+                const uint32_t room = qh - anchor < ch ? qh - anchor : ch;
+                const uint32_t cu = back_from(img, qh, ch, room);
+                const uint32_t ipm = qh - cu, cand = ch - cu;
+                const uint32_t t = count_from(img, qh, ch, 4, matchlimit, lane) + cu;
+                LZ4E_TR(2, ipm, ((uint64_t)cand << 32) | t);
+                const uint32_t L = ipm - anchor;
+                const uint32_t tok = op++;
+                if (limited && (uint64_t)op + L + 8 + L / 255 > cap) goto fail;
+                uint32_t tokhi;
+                if (L >= 15) {
+                    tokhi = 0xF0;
+                    op += out_ext(out, op, L - 15, lane);
+                } else {
+                    tokhi = L << 4;
+                }
+                out_copy(out, op, img, anchor, L, lane);
+                op += L;
+                lockstep();
+                if (!emit_match(tok, tokhi, ipm - cand, t - 4)) goto fail;
+                if (kStamps) { st.cnt[1]++; st.lap(kPhLit); }
+                e = ipm + t;
+                anchor = e;
+                rmode = true;
+                if (e > mflimit) {
+                    ip = e;
+                    goto last_literals;
+                }
+            }
         }
     }
 
@@ -633,11 +805,11 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
     if constexpr (kLdsInput) {
         uint32_t* inw = smem + kTableBytes / 4;
         stage_block(inw, in, n, lane);
-        __syncthreads();
+        block_sync();
         const LdsImage img{inw, n == 0 ? 0 : (n - 1) >> 2};
         dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane);
     } else {
-        __syncthreads();
+        block_sync();
         const HbmImage img{(gcu8*)in, n};
         dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane);
     }

@@ -96,7 +96,6 @@ LZ4E_DEV bool ugt(uint32_t a, int32_t b) { return b < 0 || a > (uint32_t)b; }
 
 constexpr uint32_t kSat = 0x7FFFFFFFu;  // length saturation: keeps every bound check's outcome
 
-LZ4E_DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 LZ4E_DEV uint4 ld16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
 LZ4E_DEV void st16(uint8_t* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
@@ -261,7 +260,7 @@ LZ4E_DEV uint32_t pack_deltas(uint32_t w) {
 // Byte at per-lane window offset x (< 512) via ds_bpermute.
 LZ4E_DEV uint32_t win_byte_lane(uint32_t a, uint32_t b, uint32_t x) {
     const uint32_t wi = x >> 2;
-    const uint32_t va = __shfl(a, (int)(wi & 63)), vb = __shfl(b, (int)(wi & 63));
+    const uint32_t va = shfl(a, (int)(wi & 63)), vb = shfl(b, (int)(wi & 63));
     return ((wi < 64 ? va : vb) >> ((x & 3) * 8)) & 0xFFu;
 }
 
@@ -269,29 +268,29 @@ LZ4E_DEV int32_t excl_scan_add(int32_t v, uint32_t lane) {
     int32_t x = v;
 #pragma unroll
     for (uint32_t d = 1; d < kWave; d <<= 1) {
-        const int32_t y = __shfl_up(x, d);
+        const int32_t y = shfl_up(x, d);
         if (lane >= d) x += y;
     }
     return x - v;
 }
 
 LZ4E_DEV int32_t excl_scan_min(int32_t v, uint32_t lane) {
-    int32_t x = __shfl_up(v, 1);
+    int32_t x = shfl_up(v, 1);
     if (lane == 0) x = INT32_MAX;
 #pragma unroll
     for (uint32_t d = 1; d < kWave; d <<= 1) {
-        const int32_t y = __shfl_up(x, d);
+        const int32_t y = shfl_up(x, d);
         if (lane >= d) x = y < x ? y : x;
     }
     return x;
 }
 
 LZ4E_DEV int32_t excl_scan_max(int32_t v, uint32_t lane) {
-    int32_t x = __shfl_up(v, 1);
+    int32_t x = shfl_up(v, 1);
     if (lane == 0) x = INT32_MIN;
 #pragma unroll
     for (uint32_t d = 1; d < kWave; d <<= 1) {
-        const int32_t y = __shfl_up(x, d);
+        const int32_t y = shfl_up(x, d);
         if (lane >= d) x = y > x ? y : x;
     }
     return x;
@@ -309,12 +308,12 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
     uint64_t st_t = 0, st_acc[3] = {0, 0, 0}, st_batches = 0, st_rounds = 0;
     auto lap = [&](int ph) {
         if constexpr (kStamps) {
-            const uint64_t now = __builtin_amdgcn_s_memtime();
+            const uint64_t now = clock64();
             st_acc[ph] += now - st_t;
             st_t = now;
         }
     };
-    if constexpr (kStamps) st_t = __builtin_amdgcn_s_memtime();
+    if constexpr (kStamps) st_t = clock64();
     const uint32_t b = blockIdx.x;
     if (b >= nblocks) return;
     const uint32_t lane = lane_id();

@@ -7,9 +7,10 @@
 
 namespace lz4e {
 
-// Largest block whose bytes are staged in LDS by the compressor (64 KiB
-// block + 16 KiB table = half a CU's LDS, two blocks per CU).
-constexpr uint32_t kMaxLdsInput = 65536;
+// Largest block whose bytes the compressor stages in LDS.  The parse is
+// latency-bound per block, so the 16 KiB table alone (10 blocks per CU,
+// input read through L1/L2) beats staging for anything but small blocks.
+constexpr uint32_t kMaxLdsInput = 4096;
 
 struct CompressBatch {
     const uint8_t* src;

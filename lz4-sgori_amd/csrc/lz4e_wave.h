@@ -1,0 +1,58 @@
+// lz4e_wave.h -- the wave64 primitives the gfx950 LZ4E kernels are written
+// against: lane identity, ballots, cross-lane reads, byte alignment, the
+// shader clock and the global-memory pointer types.  Kernel code uses only
+// these (never the amdgcn builtins directly), so the whole parse can also be
+// exercised lane-by-lane by the host-side emulator under tools/emu/, which
+// supplies its own version of this one header.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define LZ4E_DEV __device__ __forceinline__
+
+namespace lz4e {
+
+constexpr uint32_t kWave = 64;
+
+LZ4E_DEV uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+LZ4E_DEV uint64_t ballot(bool p) { return __ballot(p); }
+// v_readfirstlane: the value of the first active lane, as a scalar.
+LZ4E_DEV uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+// v_readlane: lane l's value, as a scalar (l wave-uniform).
+LZ4E_DEV uint32_t lane_val(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+// ds_bpermute: lane src's value, per lane.
+LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return __shfl(v, (int)src); }
+LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) { return __shfl_up(v, d); }
+// v_alignbyte: bytes r..r+3 of the 64-bit value hi:lo.
+LZ4E_DEV uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
+    return __builtin_amdgcn_alignbyte(hi, lo, r);
+}
+// s_memtime: shader clock (diagnostic builds only).
+LZ4E_DEV uint64_t clock64() { return __builtin_amdgcn_s_memtime(); }
+// Order this wave's LDS/global accesses (memory model fence, wavefront scope).
+LZ4E_DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+// The lanes of a wave execute in lockstep: a memory instruction completes
+// (LDS) or is ordered (global stores to one address) for every lane before
+// the wave's next one.  Marks the places that rely on it -- a whole-wave put
+// followed by a read-back, a lane's store overwriting bytes another lane
+// stored just before -- and emits no code.
+LZ4E_DEV void lockstep() {}
+// Workgroup barrier (one wave per workgroup: orders the LDS staging).
+LZ4E_DEV void block_sync() { __syncthreads(); }
+
+// Moves a (possibly wave-uniform) byte offset into a VGPR.  A uniform load
+// from read-only memory would otherwise become s_load_*, which ignores the
+// low two address bits -- wrong for unaligned reads.
+LZ4E_DEV uint32_t vaddr(uint32_t q) {
+    asm("" : "+v"(q));
+    return q;
+}
+
+// Global-memory pointer types: pointers rebuilt from integer addresses lose
+// their address space and would otherwise compile to flat_* accesses, which
+// also count on lgkmcnt (coupling them to every LDS wait).
+typedef __attribute__((address_space(1))) const uint32_t gcu32;
+typedef __attribute__((address_space(1))) const uint8_t gcu8;
+
+}  // namespace lz4e

@@ -33,17 +33,18 @@ def seqs(f):
     return out
 
 
-for g in sorted(glob.glob(os.path.join(REPO, "gpurun_out", "dbg", "*.gpu"))):
-    base = g[:-4]
-    cls = int(os.path.basename(base).split("_")[1])
-    data = open(base + ".in", "rb").read()
-    gf = open(g, "rb").read()
-    er, ef, _, _ = oracle_ref.compress(data, cls)
-    if gf == ef:
-        continue
-    a, b = seqs(gf), seqs(ef)
-    k = next((j for j in range(min(len(a), len(b))) if a[j] != b[j]), None)
-    print(os.path.basename(base), len(data), "gpu", len(gf), "ref", len(ef), "first diff seq", k)
-    if k is not None:
-        for j in range(max(0, k - 2), min(k + 3, len(a), len(b))):
-            print("   ", j, "gpu", a[j], "ref", b[j])
+if __name__ == "__main__":
+    for g in sorted(glob.glob(os.path.join(REPO, "gpurun_out", "dbg", "*.gpu"))):
+      base = g[:-4]
+      cls = int(os.path.basename(base).split("_")[1])
+      data = open(base + ".in", "rb").read()
+      gf = open(g, "rb").read()
+      er, ef, _, _ = oracle_ref.compress(data, cls)
+      if gf == ef:
+          continue
+      a, b = seqs(gf), seqs(ef)
+      k = next((j for j in range(min(len(a), len(b))) if a[j] != b[j]), None)
+      print(os.path.basename(base), len(data), "gpu", len(gf), "ref", len(ef), "first diff seq", k)
+      if k is not None:
+          for j in range(max(0, k - 2), min(k + 3, len(a), len(b))):
+              print("   ", j, "gpu", a[j], "ref", b[j])

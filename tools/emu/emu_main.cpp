@@ -1,0 +1,30 @@
+// Standalone driver of the lane emulator (for sanitizers / debuggers):
+//   emu_main BLOCK_FILE TABLE_CLASS [LDS_MAX]
+// compresses one block and prints the return value.
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <vector>
+
+extern "C" int emu_compress_batch(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
+                                  const uint8_t* table_type, uint8_t* dst, const uint64_t* dst_off,
+                                  const uint32_t* dst_cap, int32_t* ret, uint32_t* aux,
+                                  uint32_t nblocks, uint32_t max_len);
+
+int main(int argc, char** argv) {
+    FILE* f = fopen(argv[1], "rb");
+    std::vector<uint8_t> in;
+    int c;
+    while ((c = fgetc(f)) != EOF) in.push_back((uint8_t)c);
+    fclose(f);
+    const uint32_t n = (uint32_t)in.size();
+    const uint8_t tt = (uint8_t)atoi(argv[2]);
+    const uint32_t cap = n + n / 255 + 16;
+    std::vector<uint8_t> src(in), dst(cap);  // exact sizes: ASan sees any overrun
+    const uint64_t so = 0, doff = 0;
+    int32_t ret = -7;
+    uint32_t aux[2];
+    emu_compress_batch(src.data(), &so, &n, &tt, dst.data(), &doff, &cap, &ret, aux, 1, n);
+    printf("ret %d aux %u %u\n", ret, aux[0], aux[1]);
+    return 0;
+}

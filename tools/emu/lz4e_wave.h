@@ -1,0 +1,63 @@
+// Lane emulator version of csrc/lz4e_wave.h (tools/emu only): every lane of
+// the wave is a host thread; cross-lane operations meet at a barrier.  The
+// kernels call these in wave-uniform control flow only, which is what makes
+// the emulation exact (each lane executes the same sequence of them).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <barrier>
+
+#define LZ4E_DEV inline
+
+namespace lz4e {
+
+constexpr uint32_t kWave = 64;
+
+struct EmuWave {
+    std::barrier<> bar{64};
+    uint64_t slot[64];
+};
+extern EmuWave* g_wave;
+extern thread_local uint32_t g_lane;
+
+inline uint64_t emu_gather(uint64_t v, uint32_t from) {
+    g_wave->slot[g_lane] = v;
+    g_wave->bar.arrive_and_wait();
+    const uint64_t r = g_wave->slot[from & 63];
+    g_wave->bar.arrive_and_wait();
+    return r;
+}
+
+LZ4E_DEV uint32_t lane_id() { return g_lane; }
+LZ4E_DEV uint64_t ballot(bool p) {
+    g_wave->slot[g_lane] = p;
+    g_wave->bar.arrive_and_wait();
+    uint64_t m = 0;
+    for (int i = 0; i < 64; ++i) m |= (g_wave->slot[i] ? 1ull : 0ull) << i;
+    g_wave->bar.arrive_and_wait();
+    return m;
+}
+LZ4E_DEV uint32_t uni(uint32_t v) { return (uint32_t)emu_gather(v, 0); }
+LZ4E_DEV uint32_t lane_val(uint32_t v, uint32_t l) { return (uint32_t)emu_gather(v, l); }
+LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)emu_gather(v, src); }
+LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) {
+    g_wave->slot[g_lane] = (uint32_t)v;
+    g_wave->bar.arrive_and_wait();
+    const int32_t r = g_lane >= d ? (int32_t)g_wave->slot[g_lane - d] : v;
+    g_wave->bar.arrive_and_wait();
+    return r;
+}
+LZ4E_DEV uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (r & 3)));
+}
+LZ4E_DEV uint64_t clock64() { return 0; }
+LZ4E_DEV void wave_fence() {}
+LZ4E_DEV void lockstep() { g_wave->bar.arrive_and_wait(); }
+LZ4E_DEV void block_sync() { g_wave->bar.arrive_and_wait(); }
+LZ4E_DEV uint32_t vaddr(uint32_t q) { return q; }
+
+typedef const uint32_t gcu32;
+typedef const uint8_t gcu8;
+
+}  // namespace lz4e
