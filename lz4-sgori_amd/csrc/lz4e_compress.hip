@@ -392,10 +392,104 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             const uint64_t hitm = ballot(ml != 0);
             uint64_t put = 0;
             bool generic = false;
+
+            // ---- fast chain, per lane k as "rmode at B + k" --------------
+            // The common case of the walk below, precomputed for every lane
+            // at once: a rematch at k that hits (sequence with no literals,
+            // next rmode at k + ml), or one that misses followed by a search
+            // whose first probe hit j is a plain lane of this window
+            // (literals [k, j - cu), next rmode at j + ml(j)).  Anything
+            // else -- clash lanes, matches of 16+ bytes, catch-up beyond the
+            // 4 precomputed bytes, a search leaving the window, limited
+            // output -- stops the chain and the exact walk takes over.
+            // fc: next rmode lane (bits 0-6) or kStop; fe: the sequence as
+            // offset | literal length << 16 | match length << 24; fp: the
+            // puts the reference makes for it (e-2, e, the probes).
+            constexpr uint32_t kStop = 0x80;
+            uint32_t fc = kStop, fe = 0;
+            uint64_t fp = 0;
+            if (!limited) {
+                const bool plain = !((clash >> lane) & 1);
+                const int32_t lvs = (int32_t)mflimit - 1 - (int32_t)B;
+                const uint64_t inlim =
+                    lvs < 0 ? 0 : (lvs >= 63 ? ~0ull : ((2ull << (uint32_t)lvs) - 1));
+                const uint64_t srch = (lane >= 63 ? 0 : (~0ull << (lane + 1))) & inlim;
+                const uint64_t ah = hitm & ~clash & srch;
+                const uint32_t j = ah ? ctz64(ah) : 64;
+                const uint32_t jj = j < 64 ? j : lane;
+                const uint32_t mlj = shfl(ml, jj), c0j = shfl(c0, jj), bkj = shfl(bk, jj);
+                const uint64_t before_j = j < 64 ? ((1ull << j) - 1) : ~0ull;
+                const uint64_t eput = (lane >= 2 ? (1ull << (lane - 2)) : 0) | (1ull << lane);
+                if (valid && plain) {
+                    if (ml != 0) {
+                        if (!(ml & kLong)) {
+                            fc = lane + ml;
+                            fe = (p - c0) | (ml << 24);
+                            fp = eput;
+                        }
+                    } else if (j < 64 && (clash & srch & before_j) == 0 && !(mlj & kLong) &&
+                               bkj != kNoBk) {
+                        const uint32_t room = j - lane < c0j ? j - lane : c0j;
+                        const uint32_t cu = bkj < room ? bkj : room;
+                        if (!(cu == 4 && room > 4)) {
+                            fc = j + mlj;
+                            fe = (B + j - c0j) | ((j - cu - lane) << 16) | ((mlj + cu) << 24);
+                            fp = eput | lane_range(lane + 1, j);
+                        }
+                    }
+                }
+            }
             if (kStamps) { st.cnt[0]++; st.lap(kPhSearch); }
 
             // ================= walk =========================================
             for (;;) {
+                if (rmode && !limited) {
+                    // ---- fast chain: follow fc from the current rmode lane ----
+                    if (kStamps) st.lap(kPhStripe);
+                    uint32_t k = e - B, nev = 0, ev = 0;
+                    uint64_t evm = 0;
+                    while (k < 64) {
+                        const uint32_t w = lane_val(fc, k);
+                        if (w & kStop) break;
+                        ev = set_lane(ev, k, nev);
+                        put |= lane_val64(fp, k);
+                        evm |= 1ull << k;
+                        nev++;
+                        k = w;
+                    }
+                    if (nev) {
+                        // emit the nev sequences at once (lz4e_compress.c:352-453):
+                        // lane q writes sequence q's token, extension bytes and
+                        // offset; window lane x writes literal byte B + x.
+                        const uint32_t f = shfl(fe, lane < nev ? ev : 0);
+                        const uint32_t L = (f >> 16) & 0xFF, mc = (f >> 24) - 4;
+                        const uint32_t hdr = L >= 15 ? 2 : 1;
+                        const uint32_t size = lane < nev ? hdr + L + 2 + (mc >= 15 ? 1 : 0) : 0;
+                        const uint32_t o = op + excl_scan_add(size, lane);
+                        if (lane < nev) {
+                            out[o] = (uint8_t)(((L < 15 ? L : 15) << 4) | (mc < 15 ? mc : 15));
+                            if (L >= 15) out[o + 1] = (uint8_t)(L - 15);
+                            out[o + hdr + L] = (uint8_t)f;
+                            out[o + hdr + L + 1] = (uint8_t)(f >> 8);
+                            if (mc >= 15) out[o + hdr + L + 2] = (uint8_t)(mc - 15);
+                        }
+                        // literal byte of lane x: run of the last event lane s <= x
+                        const uint64_t le = evm & (lane >= 63 ? ~0ull : ((2ull << lane) - 1));
+                        const uint32_t s = le ? 63 - (uint32_t)__builtin_clzll(le) : 0;
+                        const uint32_t qi = popc64(evm & ((1ull << s) - 1));
+                        const uint32_t Lq = shfl(L, qi), dq = shfl(o + hdr, qi);
+                        if (le && lane - s < Lq) out[dq + lane - s] = (uint8_t)d0;
+                        op = lane_val(o + size, nev - 1);
+                        e = B + k;
+                        anchor = e;
+                        if (kStamps) { st.cnt[1] += nev; st.cnt[3] += nev << 16; }
+                        if (e > mflimit) {  // :456-457
+                            ip = e;
+                            goto last_literals;
+                        }
+                    }
+                }
+                if (kStamps && rmode && !limited) { st.cnt[3]++; st.lap(kPhLit); }
                 if (rmode) {
                     // ---- fill table at e-2, test e (lz4e_compress.c:461-493) ----
                     const uint32_t k = e - B;
@@ -709,7 +803,7 @@ last_literals: {
             if (lane == 0 && dbg) {
                 for (int i = 0; i < 6; ++i) dbg[i] = st.acc[i];
                 dbg[6] = ((uint64_t)st.cnt[1] << 32) | st.cnt[0];
-                dbg[7] = st.cnt[2];
+                dbg[7] = ((uint64_t)st.cnt[3] << 32) | st.cnt[2];
             }
         }
         return;

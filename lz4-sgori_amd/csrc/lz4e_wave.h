@@ -21,6 +21,10 @@ LZ4E_DEV uint64_t ballot(bool p) { return __ballot(p); }
 LZ4E_DEV uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 // v_readlane: lane l's value, as a scalar (l wave-uniform).
 LZ4E_DEV uint32_t lane_val(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
+// v with lane l (wave-uniform) set to the uniform value x.
+LZ4E_DEV uint32_t set_lane(uint32_t v, uint32_t x, uint32_t l) {
+    return lane_id() == l ? x : v;
+}
 // ds_bpermute: lane src's value, per lane.
 LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return __shfl(v, (int)src); }
 LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) { return __shfl_up(v, d); }

@@ -40,6 +40,10 @@ LZ4E_DEV uint64_t ballot(bool p) {
 }
 LZ4E_DEV uint32_t uni(uint32_t v) { return (uint32_t)emu_gather(v, 0); }
 LZ4E_DEV uint32_t lane_val(uint32_t v, uint32_t l) { return (uint32_t)emu_gather(v, l); }
+LZ4E_DEV uint32_t set_lane(uint32_t v, uint32_t x, uint32_t l) {
+    const uint32_t xx = (uint32_t)emu_gather(x, 0);  // x is wave-uniform
+    return g_lane == (l & 63) ? xx : v;
+}
 LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)emu_gather(v, src); }
 LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) {
     g_wave->slot[g_lane] = (uint32_t)v;
