@@ -10,12 +10,12 @@
 //     malformed inputs are rejected and where -- so the return value,
 //     including the error code -(ip - src) - 1, is the reference's.  The
 //     compressed bytes come from two 256-byte register windows read with
-//     v_readlane.  Sequence k of the batch is recorded in lane k (literal
-//     source, literal length, output position, offset, match length).
-//     Errors depend only on the token stream, so a failing block stops here.
-//  2. Literals: every lane copies its own run (16-byte unaligned loads and
-//     stores, exact tails); runs longer than kLong are copied by the whole
-//     wave, 1 KiB per step.
+//     v_readlane (a third is prefetched one segment ahead).  Sequence k of
+//     the batch is recorded in lane k (literal source, literal length,
+//     output position, offset, match length).  Errors depend only on the
+//     token stream, so a failing block stops here.
+//  2. Literals: every lane copies its own run; runs longer than kLong are
+//     copied by the whole wave.
 //  3. Matches, in dependency rounds: a match is ready once the part of its
 //     source before its own output overlaps no earlier match of the batch
 //     that is still pending (checked exactly against each pending interval).
@@ -25,11 +25,22 @@
 //     is what the reference's LZ4_write32(op, offset) + overlap copy produce
 //     (lz4e_decompress.c:313, 407-415).
 //
-// Same-wave stores and loads to the same global address are ordered by the
-// hardware (one vector L1 per CU); wavefront-scope fences keep the compiler
-// from moving a phase's loads above the previous phase's stores.
+// Two output placements share that loop:
+//  * LDS (blocks whose capacity is <= 64 KiB -- the 4 KiB and 64 KiB chunk
+//    sizes): the block is decoded into LDS and written to HBM once, with
+//    16-byte coalesced stores, when it is complete.  Every match copy and
+//    dependency round is then an LDS round trip, and no global store is in
+//    flight while the parse waits on its input loads (gfx9 counts loads and
+//    stores in one in-order vmcnt).  The compressed segments the parse
+//    loads are mirrored into a 1 KiB LDS ring, so literals are LDS-to-LDS
+//    copies too; the block's final literal run goes HBM-to-HBM.
+//  * HBM (larger capacities): decoded in place in the destination.  Same-
+//    wave stores and loads to the same global address are ordered by the
+//    hardware (one vector L1 per CU); wavefront-scope fences keep the
+//    compiler from moving a phase's loads above the previous phase's stores.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
 
 #include "lz4e_device.h"
 #include "lz4e_gpu.h"
@@ -40,36 +51,71 @@ namespace {
 
 constexpr int32_t kLong = 64;  // longer literal runs / matches go to the whole wave
 
-// Two 256-byte windows of the compressed block: A = [base, base+256),
-// B = [base+256, base+512).  Word loads are clamped to the block.
+// LDS per block: the input ring (+ mirror), the store sink, the span buffer.
+constexpr uint32_t kRing = 1024;                    // 4 segments of 256 B
+constexpr uint32_t kRingPad = 128;                  // mirror of ring bytes [0, 128)
+constexpr uint32_t kSink = 4 * kWave;               // a dword per lane for unwanted stores
+constexpr uint32_t kSpan = 64 * 32 + 16 + 48;       // a fast batch's output, 16-B aligned start
+
+typedef __attribute__((address_space(3))) uint8_t lu8;
+typedef __attribute__((address_space(3))) uint32_t lu32;
+typedef uint32_t __attribute__((aligned(1))) u32a1;
+typedef __attribute__((address_space(3))) u32a1 lu32a1;
+
+LZ4E_DEV uint32_t ld4(const lu8* p) { return *(const lu32a1*)p; }
+LZ4E_DEV void st4(lu8* p, uint32_t v) { *(lu32a1*)p = v; }
+
+// Two 256-byte windows of the compressed block, A = segment seg and B =
+// segment seg + 1, where segment s is block bytes [256 s - shift, +256)
+// (shift = the block's offset inside its first aligned word), plus C =
+// segment seg + 2 loaded ahead.  Word loads are clamped to the block.  With
+// a ring, every segment is written to LDS slot s & 3 when it becomes B.
 struct InWindow {
     gcu32* w;        // word-aligned base of the block
     int32_t shift;   // byte offset of the block inside w[0]
     int32_t last;    // last word index that belongs to the block
     uint32_t lane;
-    int32_t base;    // block position of window A byte 0
-    uint32_t a, b;   // this lane's dword of A and B
+    int32_t seg;     // segment of window A
+    int32_t base;    // block position of window A byte 0 (256 seg - shift)
+    int32_t ring_lo; // lowest block position held by the ring
+    uint32_t a, b, c;  // this lane's dword of A, B and C
+    lu32* ring;      // kRing + kRingPad bytes of LDS
 
     LZ4E_DEV uint32_t load(int32_t wi) const {
         wi = wi < 0 ? 0 : wi;
         return w[wi < last ? wi : last];
     }
+    LZ4E_DEV void put_ring(int32_t s, uint32_t v) const {
+        const uint32_t slot = (uint32_t)s & 3;
+        ring[slot * 64 + lane] = v;
+        if (slot == 0 && lane < kRingPad / 4) ring[kRing / 4 + lane] = v;
+    }
     LZ4E_DEV void reload(int32_t p) {
-        const int32_t wi = (p + shift) >> 2;
-        base = wi * 4 - shift;
-        a = load(wi + (int32_t)lane);
-        b = load(wi + 64 + (int32_t)lane);
+        seg = (p + shift) >> 8;
+        base = seg * 256 - shift;
+        a = load(seg * 64 + (int32_t)lane);
+        b = load(seg * 64 + 64 + (int32_t)lane);
+        c = load(seg * 64 + 128 + (int32_t)lane);
+        put_ring(seg, a);
+        put_ring(seg + 1, b);
+        ring_lo = base;
     }
     LZ4E_DEV void slide() {
         a = b;
+        b = c;
+        seg++;
         base += 256;
-        b = load(((base + shift) >> 2) + 64 + (int32_t)lane);
+        put_ring(seg + 1, b);
+        c = load(seg * 64 + 128 + (int32_t)lane);
+        const int32_t lo = base - 512;  // segments seg-2 .. seg+1 stay in the ring
+        ring_lo = ring_lo > lo ? ring_lo : lo;
     }
     // Byte p of the block (reloads when p is outside [base, base + 512)).
     LZ4E_DEV uint32_t byte(int32_t p) {
         uint32_t r = (uint32_t)(p - base);
         if (r >= 512) {
-            reload(p);
+            if (r < 768) slide();
+            else reload(p);
             r = (uint32_t)(p - base);
         }
         const uint32_t w = r < 256 ? lane_val(a, r >> 2) : lane_val(b, (r - 256) >> 2);
@@ -82,11 +128,25 @@ struct InWindow {
     }
     // Little-endian 16 bits at window offset r (r + 2 <= 512), no range check.
     LZ4E_DEV uint32_t ule16(uint32_t r) const { return ubyte(r) | (ubyte(r + 1) << 8); }
-    // Keep the parse position inside window A (prefetching B).
+    // Keep the parse position inside window A.
     LZ4E_DEV void follow(int32_t p) {
         const uint32_t r = (uint32_t)(p - base);
         if (r >= 256 && r < 512) slide();
         else if (r >= 512) reload(p);
+    }
+    // Little-endian 32 / 16 bits at block position p from the ring
+    // (p in [ring_lo, base + 512 - 4 / 2)).
+    LZ4E_DEV uint32_t rd4(int32_t p) const {
+        return ld4(reinterpret_cast<const lu8*>(ring) + ((uint32_t)(p + shift) & (kRing - 1)));
+    }
+    LZ4E_DEV uint32_t rd16(int32_t p) const { return rd4(p) & 0xFFFFu; }
+    // The ring copy of block bytes [p, p + n), or nullptr when not all held.
+    LZ4E_DEV const lu8* in_ring(int32_t p, int32_t n) const {
+        if (p < ring_lo || p + n > base + 512) return nullptr;
+        const uint32_t i = (uint32_t)(p + shift) & (kRing - 1);
+        // contiguous through the mirror, reads of up to 3 bytes past included
+        if (i + (uint32_t)n + 3 > kRing + kRingPad) return nullptr;
+        return reinterpret_cast<const lu8*>(ring) + i;
     }
 };
 
@@ -96,8 +156,24 @@ LZ4E_DEV bool ugt(uint32_t a, int32_t b) { return b < 0 || a > (uint32_t)b; }
 
 constexpr uint32_t kSat = 0x7FFFFFFFu;  // length saturation: keeps every bound check's outcome
 
+// ---------------------------------------------------------------- HBM copies
 
 LZ4E_DEV uint4 ld16(const uint8_t* p) { return *reinterpret_cast<const uint4*>(p); }
+// Global-address-space forms (flat accesses would also count on lgkmcnt,
+// coupling them to every LDS wait).
+typedef __attribute__((address_space(1))) uint8_t gu8;
+typedef __attribute__((address_space(1))) uint32_t gu32w;
+LZ4E_DEV uint4 ldg16(const uint8_t* p) {
+    const gu32w* q = (const gu32w*)p;
+    return make_uint4(q[0], q[1], q[2], q[3]);
+}
+LZ4E_DEV void stg16(uint8_t* p, uint4 v) {
+    gu32w* q = (gu32w*)p;
+    q[0] = v.x;
+    q[1] = v.y;
+    q[2] = v.z;
+    q[3] = v.w;
+}
 LZ4E_DEV void st16(uint8_t* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
 
 // Exact store of n (< 16) bytes of chunk c at p: 8/4/2/1-byte pieces.
@@ -161,10 +237,14 @@ LZ4E_DEV void lane_match(uint8_t* dst, uint32_t off, int32_t len, const uint8_t*
         return;
     }
     if (off >= 16) {
-        // self-overlap with a period >= 16: the first off bytes, then the
-        // rest from off bytes back (written just before, same lane)
+        // self-overlap with a period >= 16: the first period, then chunks
+        // copied from the start, each at most as long as what is written
         lane_copy64(dst, dst - off, (int32_t)off, lim);
-        lane_copy64(dst + off, dst, len - (int32_t)off, lim);
+        for (int32_t t = (int32_t)off; t < len;) {
+            const int32_t c = len - t < t ? len - t : t;
+            lane_copy64(dst + t, dst, c, lim);
+            t += c;
+        }
         return;
     }
     if (off == 0) {
@@ -173,11 +253,11 @@ LZ4E_DEV void lane_match(uint8_t* dst, uint32_t off, int32_t len, const uint8_t*
     }
     // 1 <= off < 16: repeat the final period [dst-off, dst) 4 bytes at a time
     // (the 16-byte load may cover bytes at/after dst: never used)
-    const uint4 p = dst - off + 16 <= lim ? ld16(dst - off) : make_uint4(0, 0, 0, 0);
     if (dst - off + 16 > lim) {
         for (int32_t t = 0; t < len; ++t) dst[t] = dst[t - (int32_t)off];
         return;
     }
+    const uint4 p = ld16(dst - off);
     uint32_t j = 0;
     int32_t t = 0;
     for (; t + 4 <= len; t += 4) {
@@ -241,100 +321,130 @@ LZ4E_DEV void wave_match(uint8_t* out, int32_t op, uint32_t off, int32_t len, ui
     }
 }
 
+// ---------------------------------------------------------------- LDS copies
+// Unaligned dword LDS accesses (gfx950 DS unaligned mode).  Sources may be
+// read up to 3 bytes past their end: the output block is followed by the
+// ring, and ring reads start below kRing with the kRingPad mirror after it.
 
-// Per lane, for each of its 4 window bytes t: the distance to the next token
-// if a token starts there and needs no length-extension bytes
-// ((t >> 4) + 3: token, literals, 2 offset bytes), else 0.  Packed 4 x 8 bits.
-LZ4E_DEV uint32_t pack_deltas(uint32_t w) {
-    uint32_t d = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t t = (w >> (8 * j)) & 0xFFu;
-        const uint32_t L = t >> 4;
-        const bool simple = L != 15 && (t & 15) != 15;
-        d |= (simple ? L + 3 : 0u) << (8 * j);
+// One piece of at most 16 bytes, src + n <= dst or another buffer: four
+// dword loads, then the stores, branch-free: a store whose bytes are not
+// all wanted goes to the lane's own dword of the sink instead.
+LZ4E_DEV void piece16(lu8* dst, const lu8* src, uint32_t n, lu8* sink) {
+    const uint32_t w0 = ld4(src), w1 = ld4(src + 4), w2 = ld4(src + 8), w3 = ld4(src + 12);
+    st4(n >= 4 ? dst : sink, w0);
+    st4(n >= 8 ? dst + 4 : sink, w1);
+    st4(n >= 12 ? dst + 8 : sink, w2);
+    st4(n >= 16 ? dst + 12 : sink, w3);
+    const uint32_t k = n & 12u, r = n & 3u;
+    const uint32_t wt = k == 0 ? w0 : (k == 4 ? w1 : (k == 8 ? w2 : w3));
+    *(r > 0 ? dst + k : sink) = (uint8_t)wt;
+    *(r > 1 ? dst + k + 1 : sink) = (uint8_t)(wt >> 8);
+    *(r > 2 ? dst + k + 2 : sink) = (uint8_t)(wt >> 16);
+}
+
+// The store half of piece16: n (<= 16) bytes of v at dst.
+LZ4E_DEV void put16(lu8* dst, uint4 v, uint32_t n, lu8* sink) {
+    st4(n >= 4 ? dst : sink, v.x);
+    st4(n >= 8 ? dst + 4 : sink, v.y);
+    st4(n >= 12 ? dst + 8 : sink, v.z);
+    st4(n >= 16 ? dst + 12 : sink, v.w);
+    const uint32_t k = n & 12u, r = n & 3u;
+    const uint32_t wt = k == 0 ? v.x : (k == 4 ? v.y : (k == 8 ? v.z : v.w));
+    *(r > 0 ? dst + k : sink) = (uint8_t)wt;
+    *(r > 1 ? dst + k + 1 : sink) = (uint8_t)(wt >> 8);
+    *(r > 2 ? dst + k + 2 : sink) = (uint8_t)(wt >> 16);
+}
+
+// len zero bytes (offset-0 matches: the reference writes zeros).
+LZ4E_DEV void lane_zero(lu8* dst, int32_t len, lu8* sink) {
+    for (int32_t t = 0; t < len; t += 16)
+        put16(dst + t, make_uint4(0, 0, 0, 0), (uint32_t)(len - t < 16 ? len - t : 16), sink);
+}
+
+// Per-lane copy of len bytes, non-overlapping, in 16-byte pieces.
+LZ4E_DEV void lane_copy(lu8* dst, const lu8* src, int32_t len, lu8* sink) {
+    for (int32_t t = 0; t < len; t += 16) {
+        const int32_t c = len - t < 16 ? len - t : 16;
+        piece16(dst + t, src + t, (uint32_t)c, sink);
     }
-    return d;
 }
 
-// Byte at per-lane window offset x (< 512) via ds_bpermute.
-LZ4E_DEV uint32_t win_byte_lane(uint32_t a, uint32_t b, uint32_t x) {
-    const uint32_t wi = x >> 2;
-    const uint32_t va = shfl(a, (int)(wi & 63)), vb = shfl(b, (int)(wi & 63));
-    return ((wi < 64 ? va : vb) >> ((x & 3) * 8)) & 0xFFu;
-}
-
-LZ4E_DEV int32_t excl_scan_add(int32_t v, uint32_t lane) {
-    int32_t x = v;
-#pragma unroll
-    for (uint32_t d = 1; d < kWave; d <<= 1) {
-        const int32_t y = shfl_up(x, d);
-        if (lane >= d) x += y;
+// Per-lane match copy of len bytes at dst with offset off >= 1 (any
+// overlap), in pieces whose source is already final: piece [t, t + c) comes
+// from D bytes back, D a multiple of off with c <= D <= t (first piece: D =
+// off, from before dst); D doubles while 2D <= t.
+LZ4E_DEV void lane_match(lu8* dst, uint32_t off, int32_t len, lu8* sink) {
+    int32_t t = 0, D = (int32_t)off;
+    while (t < len) {
+        int32_t c = len - t < 16 ? len - t : 16;
+        c = c < D ? c : D;
+        piece16(dst + t, dst + t - D, (uint32_t)c, sink);
+        t += c;
+        if (2 * D <= t) D *= 2;
     }
-    return x - v;
 }
 
-LZ4E_DEV int32_t excl_scan_min(int32_t v, uint32_t lane) {
-    int32_t x = shfl_up(v, 1);
-    if (lane == 0) x = INT32_MAX;
-#pragma unroll
-    for (uint32_t d = 1; d < kWave; d <<= 1) {
-        const int32_t y = shfl_up(x, d);
-        if (lane >= d) x = y < x ? y : x;
+// Per-lane copy of len (1..64) bytes from HBM into LDS (loads never read
+// at or past lim).
+LZ4E_DEV void lane_copy64(lu8* dst, const uint8_t* src, int32_t len, const uint8_t* lim) {
+    const uint32_t nch = ((uint32_t)len + 15) >> 4;
+    if (src + 16 * nch > lim) {
+        for (int32_t t = 0; t < len; ++t) dst[t] = src[t];
+        return;
     }
-    return x;
-}
-
-LZ4E_DEV int32_t excl_scan_max(int32_t v, uint32_t lane) {
-    int32_t x = shfl_up(v, 1);
-    if (lane == 0) x = INT32_MIN;
+    uint4 c[4];
 #pragma unroll
-    for (uint32_t d = 1; d < kWave; d <<= 1) {
-        const int32_t y = shfl_up(x, d);
-        if (lane >= d) x = y > x ? y : x;
+    for (uint32_t i = 0; i < 4; ++i) c[i] = i < nch ? ld16(src + 16 * i) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) {
+        const uint32_t w[4] = {c[i].x, c[i].y, c[i].z, c[i].w};
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+            const uint32_t k = 16 * i + 4 * j;
+            if (k + 4 <= (uint32_t)len) {
+                st4(dst + k, w[j]);
+            } else if (k < (uint32_t)len) {
+                for (uint32_t q = 0; k + q < (uint32_t)len; ++q) dst[k + q] = (uint8_t)(w[j] >> (8 * q));
+            }
+        }
     }
-    return x;
 }
 
+// ---------------------------------------------------------------- parse helpers
+
+// Byte x (< 256) of a 256-byte table held one dword per lane (ds_bpermute).
+LZ4E_DEV uint32_t table_at(uint32_t tab, uint32_t x) {
+    return (shfl(tab, x >> 2) >> ((x & 3) * 8)) & 0xFFu;
+}
+
+// The composed table B[A[p]] for this lane's 4 positions p.
+LZ4E_DEV uint32_t table_compose(uint32_t A, uint32_t B) {
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) r |= table_at(B, (A >> (8 * q)) & 0xFFu) << (8 * q);
+    return r;
+}
+
+struct Stamps {
+    uint64_t t = 0, acc[4] = {0, 0, 0, 0}, batches = 0, rounds = 0;
+};
+
+// Decode one block into HBM.  LDS: the input ring, the store sink and the
+// span buffer of the fast batches.
 template <bool kStamps>
-__global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restrict__ src,
-                                                        const uint64_t* __restrict__ src_off,
-                                                        const int32_t* __restrict__ src_len,
-                                                        uint8_t* dst,
-                                                        const uint64_t* __restrict__ dst_off,
-                                                        const int32_t* __restrict__ dst_cap,
-                                                        int32_t* __restrict__ ret, uint32_t nblocks,
-                                                        uint64_t* __restrict__ dbg) {
-    uint64_t st_t = 0, st_acc[3] = {0, 0, 0}, st_batches = 0, st_rounds = 0;
+LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, int32_t outSize,
+                           int32_t* ret_slot, uint64_t* dbg, uint32_t lane, lu8* span,
+                           lu32* ring) {
+    Stamps st;
     auto lap = [&](int ph) {
         if constexpr (kStamps) {
             const uint64_t now = clock64();
-            st_acc[ph] += now - st_t;
-            st_t = now;
+            st.acc[ph] += now - st.t;
+            st.t = now;
         }
     };
-    if constexpr (kStamps) st_t = clock64();
-    const uint32_t b = blockIdx.x;
-    if (b >= nblocks) return;
-    const uint32_t lane = lane_id();
-    const int32_t srcSize = src_len[b];
-    const int32_t outSize = dst_cap[b];
-    const uint8_t* in = src + src_off[b];
-    uint8_t* out = dst + dst_off[b];
-
-    // Special cases (lz4e_decompress.c:113-120).
-    if (outSize == 0) {
-        if (lane == 0) ret[b] = (srcSize == 1 && in[0] == 0) ? 0 : -1;
-        return;
-    }
-    if (srcSize == 0) {
-        if (lane == 0) ret[b] = -1;
-        return;
-    }
-    if (srcSize < 0) {  // token read, then every path fails at ip == 1
-        if (lane == 0) ret[b] = -2;
-        return;
-    }
+    if constexpr (kStamps) st.t = clock64();
+    lu8* sink = (lu8*)ring + kRing + kRingPad + 4 * lane;  // (span follows the sink)
 
     InWindow win;
     {
@@ -343,6 +453,7 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
         win.w = (gcu32*)(a - win.shift);
         win.last = (srcSize + win.shift - 1) >> 2;
         win.lane = lane;
+        win.ring = ring;
         win.reload(0);
     }
 
@@ -356,56 +467,68 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
         // ------------------------------------------------ 1. parse a batch
         int32_t r_ls = 0, r_L = 0, r_op = 0, r_off = 0, r_M = 0;  // lane k: sequence k
         uint32_t nseq = 0;
+        bool fastb = false;  // the batch came from the fast path (span-staged copies)
 
         // 1a. Fast path: a run of tokens with no length-extension bytes, far
         // from both block ends, where the reference takes its two-stage
-        // shortcut (:150-191).  The token chain is walked with one readlane
-        // per token; every other field and check is evaluated per lane.
+        // shortcut (:150-191).  The token chain inside the 256-byte window at
+        // ip is found by pointer doubling: jump tables J_{2^i} (window offset
+        // -> offset 2^i tokens on, 255 = chain end; one byte per position,
+        // lane l holding positions 4l..4l+3) are composed with ds_bpermute
+        // gathers, then lane k follows the bits of k to token k.  Every field
+        // and check is then evaluated per lane.
         if (ip <= iend - 18 && op <= oend - 32) {
             win.follow(ip);
-            const uint32_t r0 = (uint32_t)(ip - win.base);  // < 256
-            const uint32_t da = pack_deltas(win.a), db = pack_deltas(win.b);
-            const int32_t rin = iend - 18 - win.base;       // last token offset on the fast path
-            const uint32_t rlim = rin < 494 ? (uint32_t)rin : 494u;  // offset bytes stay inside
-            uint32_t r = r0, k = 0;
-            int32_t rk = 0;
-            while (k < kWave && r <= rlim) {
-                const uint32_t w = r < 256 ? lane_val(da, r >> 2) : lane_val(db, (r >> 2) - 64);
-                const uint32_t d = (w >> ((r & 3) * 8)) & 0xFFu;
-                if (d == 0) break;
-                rk = lane == k ? (int32_t)r : rk;
-                r += d;
-                k++;
-            }
-            if (k > 0) {
-                const bool cand = lane < k;
-                const uint32_t x = cand ? (uint32_t)rk : r0;
-                const uint32_t t = win_byte_lane(win.a, win.b, x);
-                const int32_t L = (int32_t)(t >> 4), Mt = (int32_t)(t & 15);
-                const uint32_t xo = x + 1 + (uint32_t)L;
-                const int32_t off = (int32_t)(win_byte_lane(win.a, win.b, xo) |
-                                              (win_byte_lane(win.a, win.b, xo + 1) << 8));
-                const int32_t size = cand ? L + Mt + 4 : 0;
-                const int32_t o_k = op + excl_scan_add(size, lane);
-                const int32_t m_k = o_k + L;
-                // the reference's checks on this path: shortcut entry (op <= oend-32,
-                // input side guaranteed by rlim), match inside the block (:299-302),
-                // and for offsets < 8 the _copy_match end check (:422-431)
-                const bool ok = cand && o_k <= oend - 32 && m_k >= off &&
-                                (off >= 8 || m_k + Mt + 4 <= oend - 5);
-                const uint64_t okm = ballot(ok);
-                const uint32_t nf = (~okm) ? ctz64(~okm) : kWave;  // first failing lane
-                if (nf > 0) {
-                    r_ls = win.base + (int32_t)x + 1;
-                    r_L = L;
-                    r_op = o_k;
-                    r_off = off;
-                    r_M = Mt + 4;
-                    nseq = nf;
-                    const int32_t last_end = lane_val(o_k + size, nf - 1);
-                    ip = nf < k ? win.base + lane_val(rk, nf) : win.base + (int32_t)r;
-                    op = last_end;
+            const int32_t r0 = ip - win.base;                  // < 256
+            const int32_t rin = iend - 18 - win.base;          // last token offset on the fast path
+            const int32_t jlim = (rin < 494 ? rin : 494) - r0;  // (offset bytes stay in A+B)
+            const uint32_t wv = win.rd4(ip + 4 * (int32_t)lane);
+            uint32_t J[6];
+            {
+                uint32_t j1 = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t t = (wv >> (8 * q)) & 0xFFu, p = 4 * lane + q;
+                    const uint32_t n = p + (t >> 4) + 3;
+                    const bool go = (t >> 4) != 15 && (t & 15) != 15 && (int32_t)p <= jlim && n <= 254;
+                    j1 |= (go ? n : 255u) << (8 * q);
                 }
+                J[0] = j1;
+            }
+#pragma unroll
+            for (int i = 1; i < 6; ++i) J[i] = table_compose(J[i - 1], J[i - 1]);
+            uint32_t x = 0;  // lane k: window offset of token k (255: past the chain)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) {
+                const uint32_t y = table_at(J[i], x);
+                x = (lane >> i) & 1 ? y : x;
+            }
+            const uint32_t t = table_at(wv, x);  // token byte
+            const int32_t L = (int32_t)(t >> 4), Mt = (int32_t)(t & 15);
+            const bool cand = x != 255 && L != 15 && Mt != 15 && (int32_t)x <= jlim;
+            const int32_t lp = ip + (int32_t)x + 1;  // literal start
+            const int32_t off = cand ? (int32_t)win.rd16(lp + L) : 0;
+            const int32_t size = cand ? L + Mt + 4 : 0;
+            const int32_t incl = (int32_t)wave_incl_add((uint32_t)size);
+            const int32_t o_k = op + incl - size;
+            const int32_t m_k = o_k + L;
+            // the reference's checks on this path: shortcut entry (op <= oend-32,
+            // input side guaranteed by jlim), match inside the block (:299-302),
+            // and for offsets < 8 the _copy_match end check (:422-431)
+            const bool ok = cand && o_k <= oend - 32 && m_k >= off &&
+                            (off >= 8 || m_k + Mt + 4 <= oend - 5);
+            const uint64_t okm = ballot(ok);
+            const uint32_t nf = (~okm) ? ctz64(~okm) : kWave;  // first failing lane
+            if (nf > 0) {
+                fastb = true;
+                r_ls = lp;
+                r_L = L;
+                r_op = o_k;
+                r_off = off;
+                r_M = Mt + 4;
+                nseq = nf;
+                op += lane_val((uint32_t)incl, nf - 1);
+                ip = lane_val((uint32_t)(lp + L + 2), nf - 1);  // the token after the last one
             }
         }
 
@@ -495,88 +618,195 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
             break;
         }
         lap(0);
-        if constexpr (kStamps) st_batches++;
-        // ------------------------------------------------ 2. literals
+        if constexpr (kStamps) st.batches++;
         const bool valid = lane < nseq;
+        if (fastb) {
+            // ---------------- span-staged copies (fast batches) -------------
+            // The batch's output [lo, op) (<= 64 x 32 bytes) is assembled in
+            // LDS: literals from the ring; the part of a match source that
+            // lies before lo from HBM (final: written by earlier batches);
+            // the rest in LDS dependency rounds.  Then one store pass.
+            const int32_t lo = lane_val((uint32_t)r_op, 0);
+            const int32_t a0 = lo & ~15;  // span index of position x: x - a0
+            const int32_t ms = r_op + r_L, ss = ms - r_off;
+            int32_t n0 = 0;
+            uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0;
+            if (valid && ss < lo) {  // fast path: lo <= oend - 32, so [ss, ss + 32) is in the block
+                n0 = r_M < lo - ss ? r_M : lo - ss;
+                h0 = ldg16(gout + ss);
+                if (n0 > 16) h1 = ldg16(gout + ss + 16);
+            }
+            if (valid && r_L > 0) {
+                const lu8* rs = win.in_ring(r_ls, r_L);
+                if (rs) lane_copy(span + (r_op - a0), rs, r_L, sink);
+                else lane_copy64(span + (r_op - a0), in + r_ls, r_L, in + srcSize);
+            }
+            if (n0 > 0) {
+                put16(span + (ms - a0), h0, n0 < 16 ? n0 : 16, sink);
+                if (n0 > 16) put16(span + (ms - a0) + 16, h1, n0 - 16, sink);
+            }
+            lap(1);
+            const int32_t ms2 = ms + n0, m2 = r_M - n0, me = ms + r_M;
+            const int32_t ss2 = ss + n0;
+            const int32_t need = me - r_off < ms2 ? me - r_off : ms2;  // source part before own output
+            uint64_t pending = ballot(valid && m2 > 0);
+            while (pending) {
+                // ready when [ss2, need) overlaps no earlier pending output
+                const bool mine = (pending >> lane) & 1;
+                const int32_t mn = wave_excl_min(mine ? ms2 : INT32_MAX);
+                const int32_t mx = wave_excl_max(mine ? me : INT32_MIN);
+                const bool ready = mine && (need <= mn || ss2 >= mx);
+                if (ready) {
+                    if (r_off != 0) lane_match(span + (ms2 - a0), (uint32_t)r_off, m2, sink);
+                    else lane_zero(span + (ms2 - a0), m2, sink);
+                }
+                pending &= ~ballot(ready);
+                if constexpr (kStamps) st.rounds++;
+            }
+            lap(2);
+            // store pass: 16-byte HBM chunks of [lo, op); partial end chunks by bytes
+            const int32_t nch = (op - a0 + 15) >> 4;
+            for (int32_t i = (int32_t)lane; i < nch; i += kWave) {
+                const int32_t c0 = a0 + 16 * i;
+                const lu8* sc = span + 16 * i;
+                if (c0 >= lo && c0 + 16 <= op) {
+                    stg16(gout + c0, make_uint4(ld4(sc), ld4(sc + 4), ld4(sc + 8), ld4(sc + 12)));
+                } else {
+                    for (int32_t x = c0 > lo ? c0 : lo; x < c0 + 16 && x < op; ++x)
+                        *(gu8*)(gout + x) = sc[x - c0];
+                }
+            }
+            lap(3);
+            continue;
+        }
+        // ---------------- in-HBM copies (scalar-path batches) ---------------
+        // ------------------------------------------------ 2. literals
         wave_fence();
-        if (valid && r_L > 0 && r_L <= kLong) lane_copy64(out + r_op, in + r_ls, r_L, in + srcSize);
+        if (valid && r_L > 0 && r_L <= kLong) lane_copy64(gout + r_op, in + r_ls, r_L, in + srcSize);
         {
             uint64_t longs = ballot(valid && r_L > kLong);
             while (longs) {
                 const uint32_t j = ctz64(longs);
                 longs &= longs - 1;
-                wave_copy(out + lane_val(r_op, j), in + lane_val(r_ls, j),
-                          (uint32_t)lane_val(r_L, j), lane);
+                wave_copy(gout + lane_val(r_op, j), in + lane_val(r_ls, j), (int32_t)lane_val(r_L, j),
+                          lane);
             }
         }
         wave_fence();
         lap(1);
 
         // ------------------------------------------------ 3. matches
-        const int32_t ms = r_op + r_L;  // match start
-        const int32_t me = ms + r_M;    // match end
-        const int32_t ss = ms - r_off;  // source start
-        const int32_t need = me - r_off < ms ? me - r_off : ms;  // source part before own output
-        const uint8_t* olim = out + outSize;
-        const int32_t batch_lo = lane_val(r_op, 0);
-        uint64_t pending = ballot(valid && r_M > 0);
-        while (pending) {
-            // Ready when [ss, need) is final: before this batch's output, or
-            // before every pending earlier match, or after all of them.
-            const bool mine = (pending >> lane) & 1;
-            const bool quick = need <= batch_lo;
-            bool ready = mine && quick;
-            if (ballot(mine && !quick)) {
-                const int32_t mn = excl_scan_min(mine ? ms : INT32_MAX, lane);
-                const int32_t mx = excl_scan_max(mine ? me : INT32_MIN, lane);
-                ready = mine && (quick || need <= mn || ss >= mx);
-            }
-            if (ready && r_M <= kLong) lane_match(out + ms, (uint32_t)r_off, r_M, olim);
-            wave_fence();
-            uint64_t longs = ballot(ready && r_M > kLong);
-            while (longs) {
-                const uint32_t j = ctz64(longs);
-                longs &= longs - 1;
-                wave_match(out, lane_val(ms, j), lane_val(r_off, j), (uint32_t)lane_val(r_M, j),
-                           lane);
+        {
+            const int32_t ms = r_op + r_L;  // match start
+            const int32_t me = ms + r_M;    // match end
+            const int32_t need = me - r_off < ms ? me - r_off : ms;  // source part before own output
+            const int32_t ss = ms - r_off;  // source start
+            const int32_t batch_lo = lane_val(r_op, 0);
+            uint64_t pending = ballot(valid && r_M > 0);
+            while (pending) {
+                // Ready when [ss, need) is final: before this batch's output, or
+                // before every pending earlier match, or after all of them.
+                const bool mine = (pending >> lane) & 1;
+                const bool quick = need <= batch_lo;
+                bool ready = mine && quick;
+                if (ballot(mine && !quick)) {
+                    const int32_t mn = wave_excl_min(mine ? ms : INT32_MAX);
+                    const int32_t mx = wave_excl_max(mine ? me : INT32_MIN);
+                    ready = mine && (quick || need <= mn || ss >= mx);
+                }
+                if (ready && r_M <= kLong) lane_match(gout + ms, (uint32_t)r_off, r_M, gout + outSize);
                 wave_fence();
+                uint64_t longs = ballot(ready && r_M > kLong);
+                while (longs) {
+                    const uint32_t j = ctz64(longs);
+                    longs &= longs - 1;
+                    wave_match(gout, lane_val(ms, j), lane_val(r_off, j), lane_val(r_M, j), lane);
+                    wave_fence();
+                }
+                pending &= ~ballot(ready);
+                if constexpr (kStamps) st.rounds++;
             }
-            pending &= ~ballot(ready);
-            if constexpr (kStamps) st_rounds++;
         }
         wave_fence();
         lap(2);
     }
-    if (lane == 0) ret[b] = op;
+    if (lane == 0) *ret_slot = op;
+    goto finish;
+fail:
+    if (lane == 0) *ret_slot = -ip - 1;
+finish:
     if constexpr (kStamps) {
         if (lane == 0 && dbg) {
-            uint64_t* d = dbg + 8 * (size_t)b;
-            d[0] = st_acc[0];
-            d[1] = st_acc[1];
-            d[2] = st_acc[2];
-            d[3] = st_batches;
-            d[4] = st_rounds;
+            dbg[0] = st.acc[0];
+            dbg[1] = st.acc[1];
+            dbg[2] = st.acc[2];
+            dbg[3] = st.batches;
+            dbg[4] = st.rounds;
+            dbg[5] = st.acc[3];
         }
     }
-    return;
-fail:
-    if (lane == 0) ret[b] = -ip - 1;
+}
+
+// The reference's special cases (lz4e_decompress.c:113-120); true when the
+// block is fully handled.
+LZ4E_DEV bool special_case(const uint8_t* in, int32_t srcSize, int32_t outSize, int32_t* ret_slot,
+                           uint32_t lane) {
+    if (outSize == 0) {
+        if (lane == 0) *ret_slot = (srcSize == 1 && in[0] == 0) ? 0 : -1;
+        return true;
+    }
+    if (srcSize == 0) {
+        if (lane == 0) *ret_slot = -1;
+        return true;
+    }
+    if (srcSize < 0) {  // token read, then every path fails at ip == 1
+        if (lane == 0) *ret_slot = -2;
+        return true;
+    }
+    return false;
+}
+
+template <bool kStamps>
+__global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restrict__ src,
+                                                        const uint64_t* __restrict__ src_off,
+                                                        const int32_t* __restrict__ src_len,
+                                                        uint8_t* dst,
+                                                        const uint64_t* __restrict__ dst_off,
+                                                        const int32_t* __restrict__ dst_cap,
+                                                        int32_t* __restrict__ ret, uint32_t nblocks,
+                                                        uint64_t* __restrict__ dbg) {
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks) return;
+    const uint32_t lane = lane_id();
+    const int32_t srcSize = src_len[b];
+    const int32_t outSize = dst_cap[b];
+    const uint8_t* in = src + src_off[b];
+    uint8_t* out = dst + dst_off[b];
+    uint64_t* d = kStamps && dbg ? dbg + 8 * (size_t)b : nullptr;
+    if (special_case(in, srcSize, outSize, ret + b, lane)) return;
+    // LDS: [input ring + mirror] [store sink] [span]
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kRing + kRingPad + kSink + kSpan];
+    decode_block<kStamps>(in, srcSize, out, outSize, ret + b, d, lane,
+                          (lu8*)(smem + kRing + kRingPad + kSink), (lu32*)smem);
+}
+
+template <bool kStamps>
+hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* dbg) {
+    if (a.nblocks == 0) return hipSuccess;
+    hipLaunchKernelGGL((decompress_kernel<kStamps>), dim3(a.nblocks), dim3(kWave), 0, stream,
+                       a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
+                       dbg);
+    return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t launch_decompress(const DecompressBatch& a, hipStream_t stream) {
-    if (a.nblocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(decompress_kernel<false>, dim3(a.nblocks), dim3(kWave), 0, stream, a.src,
-                       a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks, nullptr);
-    return hipGetLastError();
+    return launch_impl<false>(a, stream, nullptr);
 }
 
 hipError_t launch_decompress_stamped(const DecompressBatch& a, hipStream_t stream, uint64_t* dbg) {
-    if (a.nblocks == 0) return hipSuccess;
-    hipLaunchKernelGGL(decompress_kernel<true>, dim3(a.nblocks), dim3(kWave), 0, stream, a.src,
-                       a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks, dbg);
-    return hipGetLastError();
+    return launch_impl<true>(a, stream, dbg);
 }
 
 }  // namespace lz4e

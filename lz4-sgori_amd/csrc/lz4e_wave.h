@@ -25,9 +25,67 @@ LZ4E_DEV uint32_t lane_val(uint32_t v, uint32_t l) { return __builtin_amdgcn_rea
 LZ4E_DEV uint32_t set_lane(uint32_t v, uint32_t x, uint32_t l) {
     return lane_id() == l ? x : v;
 }
+// v_writelane: v with lane l (wave-uniform) set to the wave-uniform x.  No
+// builtin exists; gfx9 takes a variable lane select from m0 only (as the
+// compiler's own lowering of llvm.amdgcn.writelane does, m0 being set right
+// before every use), and the s_nop covers the lane-select hazard.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+LZ4E_DEV uint32_t put_lane(uint32_t v, uint32_t x, uint32_t l) {
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 4\n\tv_writelane_b32 %0, %1, m0"
+                 : "+v"(v)
+                 : "s"(x), "s"(l)
+                 : "m0");
+    return v;
+}
+#pragma clang diagnostic pop
 // ds_bpermute: lane src's value, per lane.
 LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return __shfl(v, (int)src); }
 LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) { return __shfl_up(v, d); }
+// Inclusive prefix sum over the 64 lanes with DPP (row_shr 1/2/4/8 inside
+// each row of 16, then row_bcast:15 and row_bcast:31 across rows).
+LZ4E_DEV uint32_t wave_incl_add(uint32_t v) {
+    const uint32_t lane = lane_id();
+    uint32_t x = v, t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+    x += (lane & 15) >= 1 ? t : 0u;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+    x += (lane & 15) >= 2 ? t : 0u;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+    x += (lane & 15) >= 4 ? t : 0u;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+    x += (lane & 15) >= 8 ? t : 0u;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+    x += (lane & 16) ? t : 0u;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+    x += (lane & 32) ? t : 0u;
+    return x;
+}
+// Exclusive prefix min / max over the 64 lanes (lane 0 gets the identity):
+// the DPP inclusive scan, then one lane shift.
+template <bool kMax>
+LZ4E_DEV int32_t wave_excl_minmax(int32_t v) {
+    const uint32_t lane = lane_id();
+    const int32_t id = kMax ? INT32_MIN : INT32_MAX;
+    auto op = [](int32_t a, int32_t b) { return kMax ? (a > b ? a : b) : (a < b ? a : b); };
+    int32_t x = v, t;
+    t = __builtin_amdgcn_update_dpp(id, x, 0x111, 0xf, 0xf, false);
+    x = (lane & 15) >= 1 ? op(x, t) : x;
+    t = __builtin_amdgcn_update_dpp(id, x, 0x112, 0xf, 0xf, false);
+    x = (lane & 15) >= 2 ? op(x, t) : x;
+    t = __builtin_amdgcn_update_dpp(id, x, 0x114, 0xf, 0xf, false);
+    x = (lane & 15) >= 4 ? op(x, t) : x;
+    t = __builtin_amdgcn_update_dpp(id, x, 0x118, 0xf, 0xf, false);
+    x = (lane & 15) >= 8 ? op(x, t) : x;
+    t = __builtin_amdgcn_update_dpp(id, x, 0x142, 0xa, 0xf, false);
+    x = (lane & 16) ? op(x, t) : x;
+    t = __builtin_amdgcn_update_dpp(id, x, 0x143, 0xc, 0xf, false);
+    x = (lane & 32) ? op(x, t) : x;
+    const int32_t e = __shfl_up(x, 1);
+    return lane == 0 ? id : e;
+}
+LZ4E_DEV int32_t wave_excl_min(int32_t v) { return wave_excl_minmax<false>(v); }
+LZ4E_DEV int32_t wave_excl_max(int32_t v) { return wave_excl_minmax<true>(v); }
 // v_alignbyte: bytes r..r+3 of the 64-bit value hi:lo.
 LZ4E_DEV uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
     return __builtin_amdgcn_alignbyte(hi, lo, r);

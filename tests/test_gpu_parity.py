@@ -324,3 +324,26 @@ def test_full_size_roundtrip(gpu, cls, bs, kind):
     # the oracle on every 8th block: identical frames
     for i in range(0, n_blocks, 8):
         assert frames[i] == oracle_ref.compress(blocks[i], cls)[1]
+
+
+@pytest.mark.parametrize("cap_extra", [0, 100000])
+def test_decompress_periodic_matches(gpu, cap_extra):
+    """Self-overlapping matches of every period 1..40 and lengths around
+    1x-3x the period (the overlap-copy cases), decoded through the LDS image
+    (capacity <= 64 KiB) and in HBM (larger capacity)."""
+    rng = np.random.default_rng(99)
+    frames, caps, expect = [], [], []
+    for period in range(1, 41):
+        parts = []
+        for rep in (1, 2, 3, 5, 9, 17, 40, 200):
+            parts.append(rng.integers(0, 256, 37, dtype=np.uint8).tobytes())
+            unit = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
+            parts.append((unit * (rep + 2))[:period * rep + int(rng.integers(0, period))])
+        b = b"".join(parts) + rng.integers(0, 256, 20, dtype=np.uint8).tobytes()
+        frames.append(oracle_ref.compress(b, BYU16)[1])
+        caps.append(len(b) + cap_extra)
+        expect.append(b)
+    r, outs = _gpu_decompress(gpu, frames, caps)
+    for i in range(len(frames)):
+        assert r[i] == len(expect[i]), i
+        assert outs[i] == expect[i], i

@@ -46,10 +46,10 @@ def run(name, data, bs, cls):
     torch.cuda.synchronize()
     assert torch.equal(out[:n * bs], src)
     d = dbg.cpu().numpy().reshape(n, 8).astype(np.float64)
-    tot = d[:, :3].sum(1)
+    tot = d[:, :3].sum(1) + d[:, 5]
     print(f"== {name}: {n} blocks, cycles/block mean {tot.mean():.0f} max {tot.max():.0f}; batches {d[:,3].mean():.0f} "
           f"rounds {d[:,4].mean():.0f} ({d[:,4].sum()/max(1,d[:,3].sum()):.2f}/batch); parse {d[:,0].mean():.0f} "
-          f"lit {d[:,1].mean():.0f} match {d[:,2].mean():.0f}; cycles/batch {tot.sum()/max(1,d[:,3].sum()):.0f}")
+          f"lit {d[:,1].mean():.0f} match {d[:,2].mean():.0f} flush {d[:,5].mean():.0f}; cycles/batch {tot.sum()/max(1,d[:,3].sum()):.0f}")
     by_class(name, tot, n, lambda m: f"batches {d[m,3].mean():.0f} rounds {d[m,4].mean():.0f} parse {d[m,0].mean():.0f} lit {d[m,1].mean():.0f} match {d[m,2].mean():.0f}")
 
 run("silesia64k", corpus.silesia_proxy(1024 * 65536, 0x5157), 65536, 1)

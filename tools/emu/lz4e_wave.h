@@ -6,7 +6,9 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 #include <barrier>
+#include <climits>
 
 #define LZ4E_DEV inline
 
@@ -44,11 +46,39 @@ LZ4E_DEV uint32_t set_lane(uint32_t v, uint32_t x, uint32_t l) {
     const uint32_t xx = (uint32_t)emu_gather(x, 0);  // x is wave-uniform
     return g_lane == (l & 63) ? xx : v;
 }
+LZ4E_DEV uint32_t put_lane(uint32_t v, uint32_t x, uint32_t l) {
+    const uint32_t xx = (uint32_t)emu_gather(x, 0);  // x is wave-uniform
+    return g_lane == (l & 63) ? xx : v;
+}
 LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)emu_gather(v, src); }
 LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) {
     g_wave->slot[g_lane] = (uint32_t)v;
     g_wave->bar.arrive_and_wait();
     const int32_t r = g_lane >= d ? (int32_t)g_wave->slot[g_lane - d] : v;
+    g_wave->bar.arrive_and_wait();
+    return r;
+}
+LZ4E_DEV uint32_t wave_incl_add(uint32_t v) {
+    g_wave->slot[g_lane] = v;
+    g_wave->bar.arrive_and_wait();
+    uint32_t r = 0;
+    for (uint32_t i = 0; i <= g_lane; ++i) r += (uint32_t)g_wave->slot[i];
+    g_wave->bar.arrive_and_wait();
+    return r;
+}
+LZ4E_DEV int32_t wave_excl_min(int32_t v) {
+    g_wave->slot[g_lane] = (uint32_t)v;
+    g_wave->bar.arrive_and_wait();
+    int32_t r = INT32_MAX;
+    for (uint32_t i = 0; i < g_lane; ++i) r = std::min(r, (int32_t)(uint32_t)g_wave->slot[i]);
+    g_wave->bar.arrive_and_wait();
+    return r;
+}
+LZ4E_DEV int32_t wave_excl_max(int32_t v) {
+    g_wave->slot[g_lane] = (uint32_t)v;
+    g_wave->bar.arrive_and_wait();
+    int32_t r = INT32_MIN;
+    for (uint32_t i = 0; i < g_lane; ++i) r = std::max(r, (int32_t)(uint32_t)g_wave->slot[i]);
     g_wave->bar.arrive_and_wait();
     return r;
 }
