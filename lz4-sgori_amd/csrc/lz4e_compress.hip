@@ -227,12 +227,18 @@ LZ4E_DEV uint32_t count_from(const IMG& img, uint32_t p, uint32_t c, uint32_t t,
 }
 
 // Bytes equal going backwards from p-1 / c-1, at most room (the catch-up of
-// lz4e_compress.c:339-349), a byte per step (rare paths only).
+// lz4e_compress.c:339-349): lane l compares byte l back, 64 bytes per round
+// trip.
 template <class IMG>
 LZ4E_DEV uint32_t back_from(const IMG& img, uint32_t p, uint32_t c, uint32_t room) {
-    uint32_t b = 0;
-    while (b < room && img.rd8(p - 1 - b) == img.rd8(c - 1 - b)) ++b;
-    return b;
+    const uint32_t lane = lane_id();
+    for (uint32_t b = 0; b < room; b += kWave) {
+        const uint32_t l = b + lane;
+        const bool eq = l < room && img.rd8(p - 1 - (l < room ? l : 0)) == img.rd8(c - 1 - (l < room ? l : 0));
+        const uint64_t mm = ballot(!eq);
+        if (mm) return b + ctz64(mm);
+    }
+    return room;
 }
 
 constexpr uint32_t kLong = 1u << 31;  // ml flag: 16 bytes equal, the count goes on
@@ -376,86 +382,157 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                 if (valid && dist_ok) ml = fwd16(d0, d1, d2, d3, e0, e1, e2, e3, lim);
                 if (p >= 4 && c0 >= 4) bk = back4(dm1, em1);
             }
-            uint32_t pl = kNoBk, mlp = 0, bkp = kNoBk;
+            uint32_t pl = kNoBk, mlp = 0;
             if (clash) {
                 // against the previous member of the group (bytes via ds_bpermute)
                 const uint64_t below = same & lanes_below;
                 const uint32_t src = below ? 63 - (uint32_t)__builtin_clzll(below) : lane;
-                const uint32_t fm1 = shfl(dm1, src), f0 = shfl(d0, src), f1 = shfl(d1, src),
+                const uint32_t f0 = shfl(d0, src), f1 = shfl(d1, src),
                                f2 = shfl(d2, src), f3 = shfl(d3, src);
                 if (below) {
                     pl = src;
                     if (valid) mlp = fwd16(d0, d1, d2, d3, f0, f1, f2, f3, lim);
-                    if (p >= 4 && B + src >= 4) bkp = back4(dm1, fm1);
                 }
             }
             const uint64_t hitm = ballot(ml != 0);
             uint64_t put = 0;
             bool generic = false;
+            // Match of window position B + k against the earlier window position
+            // B + cl, from the registers of both lanes (v_readlane): forward as
+            // fwd16 (0, length < 16, or 16 | kLong) and backward up to 4 bytes.
+            auto lanes_match = [&](uint32_t k, uint32_t cl, uint32_t& m, uint32_t& bb) {
+                const uint32_t lk = matchlimit - (B + k);
+                m = fwd16(lane_val(d0, k), lane_val(d1, k), lane_val(d2, k), lane_val(d3, k),
+                          lane_val(d0, cl), lane_val(d1, cl), lane_val(d2, cl), lane_val(d3, cl), lk);
+                bb = (B + k >= 4 && B + cl >= 4) ? back4(lane_val(dm1, k), lane_val(dm1, cl)) : kNoBk;
+            };
 
-            // ---- fast chain, per lane k as "rmode at B + k" --------------
-            // The common case of the walk below, precomputed for every lane
-            // at once: a rematch at k that hits (sequence with no literals,
-            // next rmode at k + ml), or one that misses followed by a search
-            // whose first probe hit j is a plain lane of this window
-            // (literals [k, j - cu), next rmode at j + ml(j)).  Anything
-            // else -- clash lanes, matches of 16+ bytes, catch-up beyond the
-            // 4 precomputed bytes, a search leaving the window, limited
-            // output -- stops the chain and the exact walk takes over.
+            // ---- fast chain tables, per lane k as "rmode at B + k" ---------
+            // The common case of the walk below, for every lane at once given
+            // each lane's candidate (vc, match vm, back bytes vb): a rematch
+            // at k that hits (sequence with no literals, next rmode at
+            // k + vm), or one that misses followed by a search whose first
+            // probe hit j is in this window (literals [k, j - cu), next rmode
+            // at j + vm(j)).  Anything else -- matches of 16+ bytes, catch-up
+            // beyond the 4 bytes in registers, a search leaving the window,
+            // limited output -- stops the chain and the exact walk takes over.
             // fc: next rmode lane (bits 0-6) or kStop; fe: the sequence as
             // offset | literal length << 16 | match length << 24; fp: the
             // puts the reference makes for it (e-2, e, the probes).
             constexpr uint32_t kStop = 0x80;
-            uint32_t fc = kStop, fe = 0;
-            uint64_t fp = 0;
-            if (!limited) {
-                const bool plain = !((clash >> lane) & 1);
-                const int32_t lvs = (int32_t)mflimit - 1 - (int32_t)B;
-                const uint64_t inlim =
-                    lvs < 0 ? 0 : (lvs >= 63 ? ~0ull : ((2ull << (uint32_t)lvs) - 1));
-                const uint64_t srch = (lane >= 63 ? 0 : (~0ull << (lane + 1))) & inlim;
-                const uint64_t ah = hitm & ~clash & srch;
+            const int32_t lvs0 = (int32_t)mflimit - 1 - (int32_t)B;
+            const uint64_t inlim0 =
+                lvs0 < 0 ? 0 : (lvs0 >= 63 ? ~0ull : ((2ull << (uint32_t)lvs0) - 1));
+            const uint64_t srch0 = (lane >= 63 ? 0 : (~0ull << (lane + 1))) & inlim0;
+            const uint64_t eput0 = (lane >= 2 ? (1ull << (lane - 2)) : 0) | (1ull << lane);
+            auto chain_tables = [&](uint32_t vc, uint32_t vm, uint32_t vb, uint32_t& fc,
+                                    uint32_t& fe, uint64_t& fp) {
+                fc = kStop;
+                fe = 0;
+                fp = 0;
+                const uint64_t ah = ballot(vm != 0) & srch0;
                 const uint32_t j = ah ? ctz64(ah) : 64;
                 const uint32_t jj = j < 64 ? j : lane;
-                const uint32_t mlj = shfl(ml, jj), c0j = shfl(c0, jj), bkj = shfl(bk, jj);
-                const uint64_t before_j = j < 64 ? ((1ull << j) - 1) : ~0ull;
-                const uint64_t eput = (lane >= 2 ? (1ull << (lane - 2)) : 0) | (1ull << lane);
-                if (valid && plain) {
-                    if (ml != 0) {
-                        if (!(ml & kLong)) {
-                            fc = lane + ml;
-                            fe = (p - c0) | (ml << 24);
-                            fp = eput;
+                const uint32_t mlj = shfl(vm, jj), cj = shfl(vc, jj), bkj = shfl(vb, jj);
+                if (valid) {
+                    if (vm != 0) {
+                        if (!(vm & kLong)) {
+                            fc = lane + vm;
+                            fe = (p - vc) | (vm << 24);
+                            fp = eput0;
                         }
-                    } else if (j < 64 && (clash & srch & before_j) == 0 && !(mlj & kLong) &&
-                               bkj != kNoBk) {
-                        const uint32_t room = j - lane < c0j ? j - lane : c0j;
+                    } else if (j < 64 && !(mlj & kLong) && bkj != kNoBk) {
+                        const uint32_t room = j - lane < cj ? j - lane : cj;
                         const uint32_t cu = bkj < room ? bkj : room;
                         if (!(cu == 4 && room > 4)) {
                             fc = j + mlj;
-                            fe = (B + j - c0j) | ((j - cu - lane) << 16) | ((mlj + cu) << 24);
-                            fp = eput | lane_range(lane + 1, j);
+                            fe = (B + j - cj) | ((j - cu - lane) << 16) | ((mlj + cu) << 24);
+                            fp = eput0 | lane_range(lane + 1, j);
                         }
                     }
                 }
-            }
+            };
+            // Tables for the snapshot candidates: exact wherever no clash lane
+            // is involved; recomputed per chain otherwise (see the walk).
+            uint32_t fc0 = kStop, fe0 = 0;
+            uint64_t fp0 = 0;
+            if (!limited) chain_tables(c0, ml, bk, fc0, fe0, fp0);
             if (kStamps) { st.cnt[0]++; st.lap(kPhSearch); }
 
             // ================= walk =========================================
             for (;;) {
                 if (rmode && !limited) {
                     // ---- fast chain: follow fc from the current rmode lane ----
+                    // With clash lanes ahead, a candidate is "the latest put of
+                    // its group before it", and the puts are the chain's own:
+                    // guess them (every lane from here on), build the tables
+                    // from the guess, follow the chain, and repeat with the
+                    // chain's puts until they reproduce the guess below the
+                    // chain's end -- that fixpoint is the reference's parse (a
+                    // candidate only depends on puts before it).
                     if (kStamps) st.lap(kPhStripe);
-                    uint32_t k = e - B, nev = 0, ev = 0;
-                    uint64_t evm = 0;
-                    while (k < 64) {
-                        const uint32_t w = lane_val(fc, k);
-                        if (w & kStop) break;
-                        ev = set_lane(ev, k, nev);
-                        put |= lane_val64(fp, k);
-                        evm |= 1ull << k;
-                        nev++;
-                        k = w;
+                    const uint32_t ks = e - B;
+                    uint32_t k = ks, nev = 0, ev = 0;
+                    uint64_t evm = 0, pch = 0;
+                    uint32_t fc = fc0, fe = fe0;
+                    uint64_t fp = fp0;
+                    if (ks < 64) {
+                        const bool dyn = (clash >> ks) != 0;
+                        uint64_t Pg = put | (1ull << (ks - 2)) | lane_range(ks, 63);
+                        constexpr uint32_t kMaxPass = 6;
+                        for (uint32_t pass = 0;; ++pass) {
+                            if (kStamps) st.cnt[2]++;
+                            if (dyn) {
+                                const uint64_t pm =
+                                    ((clash >> lane) & 1) ? (same & Pg & lanes_below) : 0;
+                                const uint32_t cl = pm ? 63 - (uint32_t)__builtin_clzll(pm) : lane;
+                                const uint32_t g0 = shfl(d0, cl), g1 = shfl(d1, cl),
+                                               g2 = shfl(d2, cl), g3 = shfl(d3, cl),
+                                               gm1 = shfl(dm1, cl);
+                                uint32_t vc = c0, vm = ml, vb = bk;
+                                if (pm) {
+                                    vc = B + cl;
+                                    vm = valid ? fwd16(d0, d1, d2, d3, g0, g1, g2, g3, lim) : 0;
+                                    vb = (p >= 4 && B + cl >= 4) ? back4(dm1, gm1) : kNoBk;
+                                }
+                                chain_tables(vc, vm, vb, fc, fe, fp);
+                            }
+                            k = ks;
+                            nev = 0;
+                            ev = 0;
+                            evm = 0;
+                            pch = 0;
+                            while (k < 64) {
+                                const uint32_t w = lane_val(fc, k);
+                                if (w & kStop) break;
+                                ev = set_lane(ev, k, nev);
+                                pch |= lane_val64(fp, k);
+                                evm |= 1ull << k;
+                                nev++;
+                                k = w;
+                            }
+                            if (!dyn) break;
+                            // Exact once every lane the chain used (rematch lanes and
+                            // search probes: its puts minus the e-2 ones) sees the
+                            // same candidate under the chain's own puts as under the
+                            // guess.
+                            const uint64_t Pn = put | pch;
+                            const uint64_t U = pch & ~(evm >> 2);
+                            const uint64_t mem = same & lanes_below;
+                            const uint64_t cg = mem & Pg, cn = mem & Pn;
+                            const bool bad = ((U >> lane) & 1) && cg != cn &&
+                                             (cg == 0 || cn == 0 ||
+                                              __builtin_clzll(cg) != __builtin_clzll(cn));
+                            if (!ballot(bad)) break;  // fixpoint
+                            if (pass + 1 == kMaxPass) {          // give up: exact walk
+                                nev = 0;
+                                k = ks;
+                                pch = 0;
+                                break;
+                            }
+                            Pg = Pn | (k >= 64 ? 0 : lane_range(k, 63));
+                        }
+                        put |= pch;
                     }
                     if (nev) {
                         // emit the nev sequences at once (lz4e_compress.c:352-453):
@@ -507,9 +584,8 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                             if (cl == lane_val(pl, k)) {
                                 m = lane_val(mlp, k);
                             } else {
-                                m = count_from(img, e, c, 0, matchlimit, lane);
-                                if (m < 4) m = 0;
-                                if (kStamps) st.cnt[2]++;
+                                uint32_t bb;
+                                lanes_match(k, cl, m, bb);
                             }
                         }
                     } else {
@@ -517,6 +593,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                         m = lane_val(ml, k);
                     }
                     put = prior | (1ull << k);
+                    if (kStamps) st.lap(kPhCount);
                     if (m == 0) {
                         // no match at e: search from e + 1 (:496-497)
                         rmode = false;
@@ -555,40 +632,30 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                 uint64_t CL = clash & rng;
                 if (A) CL &= (1ull << ctz64(A)) - 1;
                 uint32_t hk = 64, c = 0, m = 0, b = kNoBk;
-                while (CL) {
-                    // a clash lane before the first plain hit: its candidate
-                    // is the latest earlier put of its group, else c0
-                    const uint32_t k = ctz64(CL);
-                    CL &= CL - 1;
-                    const uint64_t prior = put | (k > k0 ? lane_range(k0, k - 1) : 0);
-                    const uint64_t pm = lane_val64(same, k) & prior & ((1ull << k) - 1);
-                    if (pm == 0) {
-                        c = lane_val(c0, k);
-                        m = lane_val(ml, k);
-                        b = lane_val(bk, k);
-                    } else {
-                        const uint32_t cl = 63 - (uint32_t)__builtin_clzll(pm);
-                        c = B + cl;
-                        if (cl == lane_val(pl, k)) {
-                            m = lane_val(mlp, k);
-                            b = lane_val(bkp, k);
-                        } else {
-                            m = count_from(img, B + k, c, 0, matchlimit, lane);
-                            if (m < 4) m = 0;
-                            b = kNoBk;
-                            if (kStamps) st.cnt[2]++;
-                        }
-                    }
-                    if (m) {
-                        hk = k;
-                        break;
+                // Every probe lane at once: a clash lane's candidate is the
+                // latest member of its group put before it (the window's puts
+                // so far plus this search's earlier probes), else c0; it is
+                // matched against that member's registers (ds_bpermute).
+                uint32_t vc = c0, vm = ml, vb = bk;
+                if (CL) {
+                    const bool isc = (CL >> lane) & 1;
+                    const uint64_t prior_l = put | (lane > k0 ? lane_range(k0, lane - 1) : 0);
+                    const uint64_t pm = isc ? (same & prior_l & lanes_below) : 0;
+                    const uint32_t cl = pm ? 63 - (uint32_t)__builtin_clzll(pm) : lane;
+                    const uint32_t g0 = shfl(d0, cl), g1 = shfl(d1, cl), g2 = shfl(d2, cl),
+                                   g3 = shfl(d3, cl), gm1 = shfl(dm1, cl);
+                    if (pm) {
+                        vc = B + cl;
+                        vm = fwd16(d0, d1, d2, d3, g0, g1, g2, g3, lim);
+                        vb = (p >= 4 && B + cl >= 4) ? back4(dm1, gm1) : kNoBk;
                     }
                 }
-                if (hk == 64 && A) {
-                    hk = ctz64(A);
-                    c = lane_val(c0, hk);
-                    m = lane_val(ml, hk);
-                    b = lane_val(bk, hk);
+                const uint64_t H = ballot((((CL | A) >> lane) & 1) && vm != 0);
+                if (H) {
+                    hk = ctz64(H);
+                    c = lane_val(vc, hk);
+                    m = lane_val(vm, hk);
+                    b = lane_val(vb, hk);
                 }
                 if (hk == 64) {
                     // no hit among this window's probes: all of them put
@@ -606,6 +673,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                     continue;  // next window
                 }
                 put |= lane_range(k0, hk);
+                if (kStamps) st.lap(kPhStripe);
                 const uint32_t q = B + hk;
                 // catch up (lz4e_compress.c:339-349)
                 const uint32_t room = q - anchor < c ? q - anchor : c;
@@ -642,7 +710,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                 op += L;
                 lockstep();  // the offset overwrites the copy's spare bytes
                 if (!emit_match(tok, tokhi, ipm - cand, t - 4)) goto fail;
-                if (kStamps) st.cnt[1]++;
+                if (kStamps) { st.cnt[1]++; st.lap(kPhTail); }
                 e = ipm + t;
                 anchor = e;
                 rmode = true;

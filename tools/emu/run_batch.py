@@ -28,6 +28,8 @@ def _corpus(kind, n, seed):
         return corpus._int_table(n, rng)
     if kind == "fio":
         return corpus.fio_pattern(n, seed)
+    if kind == "records":
+        return corpus._records(n, rng)
     if kind == "small_alpha":
         return rng.integers(0, 3, n, dtype=np.uint8)
     return corpus.silesia_proxy(n, seed)

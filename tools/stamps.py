@@ -53,7 +53,7 @@ def run(name, data, bs, cls, label):
         assert r == 0
     torch.cuda.synchronize()
     d = dbg.cpu().numpy().reshape(n, 8).astype(np.float64)
-    ph = ["search", "slowwalk", "fastchain", "count", "commit", "tail"]
+    ph = ["setup", "srch_walk", "fastchain", "rmode", "commit", "srch_emit"]
     srch = d[:, 6].astype(np.int64) & 0xFFFFFFFF
     seqs = d[:, 6].astype(np.int64) >> 32
     rem = d[:, 7].astype(np.int64) & 0xFFFFFFFF
@@ -61,11 +61,11 @@ def run(name, data, bs, cls, label):
     fa, fev = (c3 & 0xFFFF), (c3 >> 16)
     tot = d[:, :6].sum(1)
     print(f"== {name} {label}: {n} blocks, mean cycles/block {tot.mean():.0f}, max {tot.max():.0f}; "
-          f"seq/block {seqs.mean():.0f} searches {srch.mean():.0f} rematch {rem.mean():.0f}; "
+          f"seq/block {seqs.mean():.0f} searches {srch.mean():.0f} passes {rem.mean():.0f}; "
           f"cycles/seq {tot.sum() / max(1, seqs.sum()):.0f}; fast attempts {fa.mean():.0f} fast seqs {fev.mean():.0f}")
     for i, p in enumerate(ph):
         print(f"   {p:8s} {d[:, i].mean():12.0f}  ({100 * d[:, i].sum() / tot.sum():5.1f}%)")
-    by_class(name, tot, n, lambda m: f"seq {seqs[m].mean():.0f} srch {srch[m].mean():.0f} " + " ".join(f"{ph[i]}={d[m, i].mean():.0f}" for i in range(5)))
+    by_class(name, tot, n, lambda m: f"seq {seqs[m].mean():.0f} srch {srch[m].mean():.0f} " + " ".join(f"{ph[i]}={d[m, i].mean():.0f}" for i in range(6)))
 
 if __name__ == "__main__":
     mode = os.environ.get("LZ4E_COMPRESS_LDS_MAX", "default")
