@@ -241,22 +241,23 @@ LZ4E_DEV uint32_t back_from(const IMG& img, uint32_t p, uint32_t c, uint32_t roo
     return room;
 }
 
-constexpr uint32_t kLong = 1u << 31;  // ml flag: 16 bytes equal, the count goes on
+constexpr uint32_t kFwdW = 8;            // dwords of forward bytes held per position
+constexpr uint32_t kFwd = 4 * kFwdW;      // 32 bytes: matches shorter than this stay in registers
+constexpr uint32_t kLong = 1u << 31;  // ml flag: kFwd bytes equal, the count goes on
 constexpr uint32_t kNoBk = 0xFF;   // bk: backward bytes not available in registers
 
-// Forward match of the 16 bytes a[] against b[], lane-wise: 0 if the first 4
-// bytes differ, the matched length capped at lim, or 16 | kLong.
-LZ4E_DEV uint32_t fwd16(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t b0,
-                        uint32_t b1, uint32_t b2, uint32_t b3, uint32_t lim) {
-    const uint32_t x0 = a0 ^ b0, x1 = a1 ^ b1, x2 = a2 ^ b2, x3 = a3 ^ b3;
-    if (x0) return 0;
-    uint32_t m;
-    if (x1) m = 4 + ((uint32_t)__builtin_ctz(x1) >> 3);
-    else if (x2) m = 8 + ((uint32_t)__builtin_ctz(x2) >> 3);
-    else if (x3) m = 12 + ((uint32_t)__builtin_ctz(x3) >> 3);
-    else m = 16;
+// Forward match of the kFwd bytes a[] against b[], lane-wise: 0 if the first
+// 4 bytes differ, the matched length capped at lim, or kFwd | kLong.
+LZ4E_DEV uint32_t fwd_match(const uint32_t* a, const uint32_t* b, uint32_t lim) {
+    if (a[0] != b[0]) return 0;
+    uint32_t m = kFwd;
+#pragma unroll
+    for (int i = (int)kFwdW - 1; i >= 1; --i) {
+        const uint32_t x = a[i] ^ b[i];
+        if (x) m = 4 * (uint32_t)i + ((uint32_t)__builtin_ctz(x) >> 3);
+    }
     if (m >= lim) return lim;
-    return m == 16 ? (16 | kLong) : m;
+    return m == kFwd ? (kFwd | kLong) : m;
 }
 
 // Equal bytes at the top of two dwords (backward catch-up, up to 4).
@@ -278,7 +279,7 @@ LZ4E_DEV uint64_t lane_range(uint32_t a, uint32_t b) {
 //
 // Window setup (all lanes at once): the 20 bytes around each position, its
 // hash, the table entry before the window (c0, the "snapshot"), the forward
-// match against c0 (ml, up to 16 bytes) and the bytes equal before both
+// match against c0 (ml, up to kFwd = 32 bytes) and the bytes equal before both
 // (bk).  Positions sharing a hash inside the window form clash groups
 // (speculative put + read-back); for those the same quantities are also
 // taken against the previous group member (mlp, bkp).
@@ -349,10 +350,12 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             const uint32_t B = rmode ? e - 2 : e;
             const uint32_t p = B + lane;
             const bool valid = p <= mflimit;  // every put / lookup is at <= mflimit
-            const uint32_t dm1 = img.ld32(clampq(p - 4)), d0 = img.ld32(clampq(p)),
-                           d1 = img.ld32(clampq(p + 4)), d2 = img.ld32(clampq(p + 8)),
-                           d3 = img.ld32(clampq(p + 12));
-            const uint32_t h = hash_val<TT>(((uint64_t)d1 << 32) | d0);
+            const uint32_t dm1 = img.ld32(clampq(p - 4));
+            uint32_t dv[kFwdW];  // bytes p .. p + kFwd - 1
+#pragma unroll
+            for (uint32_t i = 0; i < kFwdW; ++i) dv[i] = img.ld32(clampq(p + 4 * i));
+            const uint32_t d0 = dv[0];
+            const uint32_t h = hash_val<TT>(((uint64_t)dv[1] << 32) | d0);
             uint32_t c0 = 0, rb = p;
             lockstep();  // the previous window's commit is in the table
             if (valid) c0 = T.get(h);  // snapshot
@@ -375,11 +378,12 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             const uint32_t lim = matchlimit - p;
             uint32_t ml = 0, bk = kNoBk;
             {
-                const uint32_t em1 = img.ld32(clampq(c0 - 4)), e0 = img.ld32(c0),
-                               e1 = img.ld32(clampq(c0 + 4)), e2 = img.ld32(clampq(c0 + 8)),
-                               e3 = img.ld32(clampq(c0 + 12));
+                const uint32_t em1 = img.ld32(clampq(c0 - 4));
+                uint32_t ev[kFwdW];
+#pragma unroll
+                for (uint32_t i = 0; i < kFwdW; ++i) ev[i] = img.ld32(clampq(c0 + 4 * i));
                 const bool dist_ok = (TT == kByU16) || (c0 + kMaxDistance >= p);
-                if (valid && dist_ok) ml = fwd16(d0, d1, d2, d3, e0, e1, e2, e3, lim);
+                if (valid && dist_ok) ml = fwd_match(dv, ev, lim);
                 if (p >= 4 && c0 >= 4) bk = back4(dm1, em1);
             }
             uint32_t pl = kNoBk, mlp = 0;
@@ -387,11 +391,12 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                 // against the previous member of the group (bytes via ds_bpermute)
                 const uint64_t below = same & lanes_below;
                 const uint32_t src = below ? 63 - (uint32_t)__builtin_clzll(below) : lane;
-                const uint32_t f0 = shfl(d0, src), f1 = shfl(d1, src),
-                               f2 = shfl(d2, src), f3 = shfl(d3, src);
+                uint32_t fv[kFwdW];
+#pragma unroll
+                for (uint32_t i = 0; i < kFwdW; ++i) fv[i] = shfl(dv[i], src);
                 if (below) {
                     pl = src;
-                    if (valid) mlp = fwd16(d0, d1, d2, d3, f0, f1, f2, f3, lim);
+                    if (valid) mlp = fwd_match(dv, fv, lim);
                 }
             }
             const uint64_t hitm = ballot(ml != 0);
@@ -399,11 +404,16 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             bool generic = false;
             // Match of window position B + k against the earlier window position
             // B + cl, from the registers of both lanes (v_readlane): forward as
-            // fwd16 (0, length < 16, or 16 | kLong) and backward up to 4 bytes.
+            // fwd_match (0, length < kFwd, or kFwd | kLong) and backward up to 4 bytes.
             auto lanes_match = [&](uint32_t k, uint32_t cl, uint32_t& m, uint32_t& bb) {
                 const uint32_t lk = matchlimit - (B + k);
-                m = fwd16(lane_val(d0, k), lane_val(d1, k), lane_val(d2, k), lane_val(d3, k),
-                          lane_val(d0, cl), lane_val(d1, cl), lane_val(d2, cl), lane_val(d3, cl), lk);
+                uint32_t ak[kFwdW], ac[kFwdW];
+#pragma unroll
+                for (uint32_t i = 0; i < kFwdW; ++i) {
+                    ak[i] = lane_val(dv[i], k);
+                    ac[i] = lane_val(dv[i], cl);
+                }
+                m = fwd_match(ak, ac, lk);
                 bb = (B + k >= 4 && B + cl >= 4) ? back4(lane_val(dm1, k), lane_val(dm1, cl)) : kNoBk;
             };
 
@@ -486,13 +496,14 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                                 const uint64_t pm =
                                     ((clash >> lane) & 1) ? (same & Pg & lanes_below) : 0;
                                 const uint32_t cl = pm ? 63 - (uint32_t)__builtin_clzll(pm) : lane;
-                                const uint32_t g0 = shfl(d0, cl), g1 = shfl(d1, cl),
-                                               g2 = shfl(d2, cl), g3 = shfl(d3, cl),
-                                               gm1 = shfl(dm1, cl);
+                                uint32_t gv[kFwdW];
+#pragma unroll
+                                for (uint32_t i = 0; i < kFwdW; ++i) gv[i] = shfl(dv[i], cl);
+                                const uint32_t gm1 = shfl(dm1, cl);
                                 uint32_t vc = c0, vm = ml, vb = bk;
                                 if (pm) {
                                     vc = B + cl;
-                                    vm = valid ? fwd16(d0, d1, d2, d3, g0, g1, g2, g3, lim) : 0;
+                                    vm = valid ? fwd_match(dv, gv, lim) : 0;
                                     vb = (p >= 4 && B + cl >= 4) ? back4(dm1, gm1) : kNoBk;
                                 }
                                 chain_tables(vc, vm, vb, fc, fe, fp);
@@ -602,7 +613,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                         continue;
                     }
                     uint32_t t = m & ~kLong;
-                    if (m & kLong) t = count_from(img, e, c, 16, matchlimit, lane);
+                    if (m & kLong) t = count_from(img, e, c, kFwd, matchlimit, lane);
                     LZ4E_TR(2, e, ((uint64_t)c << 32) | t);
                     const uint32_t tok = op++;
                     if (!emit_match(tok, 0, e - c, t - 4)) goto fail;
@@ -642,11 +653,13 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                     const uint64_t prior_l = put | (lane > k0 ? lane_range(k0, lane - 1) : 0);
                     const uint64_t pm = isc ? (same & prior_l & lanes_below) : 0;
                     const uint32_t cl = pm ? 63 - (uint32_t)__builtin_clzll(pm) : lane;
-                    const uint32_t g0 = shfl(d0, cl), g1 = shfl(d1, cl), g2 = shfl(d2, cl),
-                                   g3 = shfl(d3, cl), gm1 = shfl(dm1, cl);
+                    uint32_t gv[kFwdW];
+#pragma unroll
+                    for (uint32_t i = 0; i < kFwdW; ++i) gv[i] = shfl(dv[i], cl);
+                    const uint32_t gm1 = shfl(dm1, cl);
                     if (pm) {
                         vc = B + cl;
-                        vm = fwd16(d0, d1, d2, d3, g0, g1, g2, g3, lim);
+                        vm = fwd_match(dv, gv, lim);
                         vb = (p >= 4 && B + cl >= 4) ? back4(dm1, gm1) : kNoBk;
                     }
                 }
@@ -686,7 +699,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                 }
                 const uint32_t ipm = q - cu, cand = c - cu;
                 uint32_t t = m & ~kLong;
-                if (m & kLong) t = count_from(img, q, c, 16, matchlimit, lane);
+                if (m & kLong) t = count_from(img, q, c, kFwd, matchlimit, lane);
                 t += cu;
                 LZ4E_TR(2, ipm, ((uint64_t)cand << 32) | t);
                 // literals [anchor, ipm) (lz4e_compress.c:352-382)
