@@ -427,19 +427,18 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             // beyond the 4 bytes in registers, a search leaving the window,
             // limited output -- stops the chain and the exact walk takes over.
             // fc: next rmode lane (bits 0-6) or kStop; fe: the sequence as
-            // offset | literal length << 16 | match length << 24; fp: the
-            // puts the reference makes for it (e-2, e, the probes).
+            // offset | literal length << 16 | match length << 24; jv: the
+            // last probe of its search (probes (k, jv]), else k.
             constexpr uint32_t kStop = 0x80;
             const int32_t lvs0 = (int32_t)mflimit - 1 - (int32_t)B;
             const uint64_t inlim0 =
                 lvs0 < 0 ? 0 : (lvs0 >= 63 ? ~0ull : ((2ull << (uint32_t)lvs0) - 1));
             const uint64_t srch0 = (lane >= 63 ? 0 : (~0ull << (lane + 1))) & inlim0;
-            const uint64_t eput0 = (lane >= 2 ? (1ull << (lane - 2)) : 0) | (1ull << lane);
             auto chain_tables = [&](uint32_t vc, uint32_t vm, uint32_t vb, uint32_t& fc,
-                                    uint32_t& fe, uint64_t& fp) {
+                                    uint32_t& fe, uint32_t& jv) {
                 fc = kStop;
                 fe = 0;
-                fp = 0;
+                jv = lane;
                 const uint64_t ah = ballot(vm != 0) & srch0;
                 const uint32_t j = ah ? ctz64(ah) : 64;
                 const uint32_t jj = j < 64 ? j : lane;
@@ -449,7 +448,6 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                         if (!(vm & kLong)) {
                             fc = lane + vm;
                             fe = (p - vc) | (vm << 24);
-                            fp = eput0;
                         }
                     } else if (j < 64 && !(mlj & kLong) && bkj != kNoBk) {
                         const uint32_t room = j - lane < cj ? j - lane : cj;
@@ -457,16 +455,15 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                         if (!(cu == 4 && room > 4)) {
                             fc = j + mlj;
                             fe = (B + j - cj) | ((j - cu - lane) << 16) | ((mlj + cu) << 24);
-                            fp = eput0 | lane_range(lane + 1, j);
+                            jv = j;
                         }
                     }
                 }
             };
             // Tables for the snapshot candidates: exact wherever no clash lane
             // is involved; recomputed per chain otherwise (see the walk).
-            uint32_t fc0 = kStop, fe0 = 0;
-            uint64_t fp0 = 0;
-            if (!limited) chain_tables(c0, ml, bk, fc0, fe0, fp0);
+            uint32_t fc0 = kStop, fe0 = 0, jv0 = lane;
+            if (!limited) chain_tables(c0, ml, bk, fc0, fe0, jv0);
             if (kStamps) { st.cnt[0]++; st.lap(kPhSearch); }
 
             // ================= walk =========================================
@@ -484,8 +481,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                     const uint32_t ks = e - B;
                     uint32_t k = ks, nev = 0, ev = 0;
                     uint64_t evm = 0, pch = 0;
-                    uint32_t fc = fc0, fe = fe0;
-                    uint64_t fp = fp0;
+                    uint32_t fc = fc0, fe = fe0, jv = jv0;
                     if (ks < 64) {
                         const bool dyn = (clash >> ks) != 0;
                         uint64_t Pg = put | (1ull << (ks - 2)) | lane_range(ks, 63);
@@ -506,21 +502,25 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                                     vm = valid ? fwd_match(dv, gv, lim) : 0;
                                     vb = (p >= 4 && B + cl >= 4) ? back4(dm1, gm1) : kNoBk;
                                 }
-                                chain_tables(vc, vm, vb, fc, fe, fp);
+                                chain_tables(vc, vm, vb, fc, fe, jv);
                             }
+                            if (kStamps) st.lap(kPhCount);
                             k = ks;
-                            nev = 0;
-                            ev = 0;
                             evm = 0;
-                            pch = 0;
-                            while (k < 64) {
+                            while (k < 64) {  // the serial part: one readlane per event
                                 const uint32_t w = lane_val(fc, k);
                                 if (w & kStop) break;
-                                ev = set_lane(ev, k, nev);
-                                pch |= lane_val64(fp, k);
                                 evm |= 1ull << k;
-                                nev++;
                                 k = w;
+                            }
+                            nev = popc64(evm);
+                            // the chain's puts (e-2 and e of every event, the probes
+                            // (l, jv(l)] of its searches), all lanes at once
+                            {
+                                const uint64_t eb = evm & lanes_below;
+                                const uint32_t lb = eb ? 63 - (uint32_t)__builtin_clzll(eb) : lane;
+                                const uint32_t jl = shfl(jv, lb);
+                                pch = ballot(eb != 0 && lane <= jl) | evm | (evm >> 2);
                             }
                             if (!dyn) break;
                             // Exact once every lane the chain used (rematch lanes and
@@ -544,7 +544,11 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                             Pg = Pn | (k >= 64 ? 0 : lane_range(k, 63));
                         }
                         put |= pch;
+                        // ev: lane q < nev holds the lane of event q
+                        const bool isev = (evm >> lane) & 1;
+                        ev = push_lane(lane, isev ? popc64(evm & lanes_below) : 63);
                     }
+                    if (kStamps) st.lap(kPhLit);
                     if (nev) {
                         // emit the nev sequences at once (lz4e_compress.c:352-453):
                         // lane q writes sequence q's token, extension bytes and
@@ -553,7 +557,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                         const uint32_t L = (f >> 16) & 0xFF, mc = (f >> 24) - 4;
                         const uint32_t hdr = L >= 15 ? 2 : 1;
                         const uint32_t size = lane < nev ? hdr + L + 2 + (mc >= 15 ? 1 : 0) : 0;
-                        const uint32_t o = op + excl_scan_add(size, lane);
+                        const uint32_t o = op + wave_incl_add(size) - size;
                         if (lane < nev) {
                             out[o] = (uint8_t)(((L < 15 ? L : 15) << 4) | (mc < 15 ? mc : 15));
                             if (L >= 15) out[o + 1] = (uint8_t)(L - 15);
@@ -570,7 +574,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                         op = lane_val(o + size, nev - 1);
                         e = B + k;
                         anchor = e;
-                        if (kStamps) { st.cnt[1] += nev; st.cnt[3] += nev << 16; }
+                        if (kStamps) { st.cnt[1] += nev; st.cnt[3] += nev << 16; st.lap(kPhTail); }
                         if (e > mflimit) {  // :456-457
                             ip = e;
                             goto last_literals;

@@ -38,15 +38,4 @@ LZ4E_DEV uint64_t probe_offset(uint32_t P) {
 }
 LZ4E_DEV uint32_t probe_step(uint32_t P) { return P == 0 ? 1u : (P + 63) >> 6; }
 
-// Exclusive prefix sum over the 64 lanes.
-LZ4E_DEV uint32_t excl_scan_add(uint32_t v, uint32_t lane) {
-    uint32_t x = v;
-#pragma unroll
-    for (uint32_t d = 1; d < kWave; d <<= 1) {
-        const uint32_t y = (uint32_t)shfl_up((int32_t)x, d);
-        if (lane >= d) x += y;
-    }
-    return x - v;
-}
-
 }  // namespace lz4e

@@ -39,6 +39,11 @@ LZ4E_DEV uint32_t put_lane(uint32_t v, uint32_t x, uint32_t l) {
     return v;
 }
 #pragma clang diagnostic pop
+// ds_permute: lane l sends v to lane dst (l's own choice); a lane nobody
+// sends to receives an unspecified value.
+LZ4E_DEV uint32_t push_lane(uint32_t v, uint32_t dst) {
+    return (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)v);
+}
 // ds_bpermute: lane src's value, per lane.
 LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return __shfl(v, (int)src); }
 LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) { return __shfl_up(v, d); }

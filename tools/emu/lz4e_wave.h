@@ -50,6 +50,16 @@ LZ4E_DEV uint32_t put_lane(uint32_t v, uint32_t x, uint32_t l) {
     const uint32_t xx = (uint32_t)emu_gather(x, 0);  // x is wave-uniform
     return g_lane == (l & 63) ? xx : v;
 }
+LZ4E_DEV uint32_t push_lane(uint32_t v, uint32_t dst) {
+    // every lane publishes (dst, v); lane l takes the value of a sender to it
+    g_wave->slot[g_lane] = ((uint64_t)(dst & 63) << 32) | v;
+    g_wave->bar.arrive_and_wait();
+    uint32_t r = 0xDEADBEEFu;
+    for (int i = 0; i < 64; ++i)
+        if ((g_wave->slot[i] >> 32) == g_lane) r = (uint32_t)g_wave->slot[i];
+    g_wave->bar.arrive_and_wait();
+    return r;
+}
 LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)emu_gather(v, src); }
 LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) {
     g_wave->slot[g_lane] = (uint32_t)v;

@@ -53,7 +53,7 @@ def run(name, data, bs, cls, label):
         assert r == 0
     torch.cuda.synchronize()
     d = dbg.cpu().numpy().reshape(n, 8).astype(np.float64)
-    ph = ["setup", "srch_walk", "fastchain", "rmode", "commit", "srch_emit"]
+    ph = ["setup", "slowwalk", "chainwalk", "tables", "commit", "emit"]
     srch = d[:, 6].astype(np.int64) & 0xFFFFFFFF
     seqs = d[:, 6].astype(np.int64) >> 32
     rem = d[:, 7].astype(np.int64) & 0xFFFFFFFF
