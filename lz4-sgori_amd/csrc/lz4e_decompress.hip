@@ -361,6 +361,27 @@ LZ4E_DEV void lane_zero(lu8* dst, int32_t len, lu8* sink) {
         put16(dst + t, make_uint4(0, 0, 0, 0), (uint32_t)(len - t < 16 ? len - t : 16), sink);
 }
 
+// The matches of lanes in `pending`, in lane order, each copied by the whole
+// wave: out[x] = out[x - off] for the match's bytes, min(off, 64) bytes per
+// step so that every source byte is final when read (offset 0 writes zeros).
+// Span index of position x: x - a0.
+LZ4E_DEV void serial_matches(lu8* span, int32_t a0, uint64_t pending, int32_t ms, int32_t m,
+                             int32_t off, uint32_t lane) {
+    while (pending) {
+        const uint32_t q = ctz64(pending);
+        pending &= pending - 1;
+        const int32_t qms = (int32_t)lane_val((uint32_t)ms, q) - a0;
+        const int32_t qm = (int32_t)lane_val((uint32_t)m, q);
+        const int32_t qoff = (int32_t)lane_val((uint32_t)off, q);
+        int32_t step = qoff == 0 || qoff > (int32_t)kWave ? (int32_t)kWave : qoff;
+        for (int32_t t0 = 0; t0 < qm; t0 += step) {
+            const int32_t t = t0 + (int32_t)lane;
+            if ((int32_t)lane < step && t < qm)
+                span[qms + t] = qoff ? span[qms - qoff + t] : (uint8_t)0;
+        }
+    }
+}
+
 // Per-lane copy of len bytes, non-overlapping, in 16-byte pieces.
 LZ4E_DEV void lane_copy(lu8* dst, const lu8* src, int32_t len, lu8* sink) {
     for (int32_t t = 0; t < len; t += 16) {
@@ -656,11 +677,21 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
                 const int32_t mn = wave_excl_min(mine ? ms2 : INT32_MAX);
                 const int32_t mx = wave_excl_max(mine ? me : INT32_MIN);
                 const bool ready = mine && (need <= mn || ss2 >= mx);
+                const uint64_t rm = ballot(ready);
+                if (rm == (pending & (0 - pending)) && (pending & (pending - 1))) {
+                    // A dependency chain (only the first pending match is
+                    // ready): copy the pending matches one after another in
+                    // lane order, each by the whole wave (lane t: byte t).
+                    serial_matches(span, a0, pending, ms2, m2, r_off, lane);
+                    if constexpr (kStamps) st.rounds += popc64(pending);
+                    pending = 0;
+                    break;
+                }
                 if (ready) {
                     if (r_off != 0) lane_match(span + (ms2 - a0), (uint32_t)r_off, m2, sink);
                     else lane_zero(span + (ms2 - a0), m2, sink);
                 }
-                pending &= ~ballot(ready);
+                pending &= ~rm;
                 if constexpr (kStamps) st.rounds++;
             }
             lap(2);
