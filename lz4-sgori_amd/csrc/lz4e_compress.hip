@@ -281,8 +281,8 @@ LZ4E_DEV uint64_t lane_range(uint32_t a, uint32_t b) {
 // hash, the table entry before the window (c0, the "snapshot"), the forward
 // match against c0 (ml, up to kFwd = 32 bytes) and the bytes equal before both
 // (bk).  Positions sharing a hash inside the window form clash groups
-// (speculative put + read-back); for those the same quantities are also
-// taken against the previous group member (mlp, bkp).
+// (speculative put + read-back); their candidates depend on the walk's own
+// puts (fixpoint chain / exact walk below).
 //
 // Walk (wave-uniform, mostly SALU): the reference parse over the window,
 // reading the precomputed lanes with v_readlane.  The candidate of a
@@ -345,8 +345,10 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
         uint32_t e = 1;      // next position of the walk
         uint32_t s = 1;      // start of the current search
         uint32_t jb = 0;     // probes of the current search done so far
+        uint32_t pf = 0;     // prefetch of the next window's bytes (warms L1/L2)
         for (;;) {
             // ================= window setup =================================
+            consume(pf);
             const uint32_t B = rmode ? e - 2 : e;
             const uint32_t p = B + lane;
             const bool valid = p <= mflimit;  // every put / lookup is at <= mflimit
@@ -359,6 +361,11 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             uint32_t c0 = 0, rb = p;
             lockstep();  // the previous window's commit is in the table
             if (valid) c0 = T.get(h);  // snapshot
+            // the snapshot candidate's bytes: issued now, used after the clash groups
+            const uint32_t em1 = img.ld32(clampq(c0 - 4));
+            uint32_t ev[kFwdW];
+#pragma unroll
+            for (uint32_t i = 0; i < kFwdW; ++i) ev[i] = img.ld32(clampq(c0 + 4 * i));
             lockstep();
             if (valid) T.put(h, p);  // speculative put of every position
             lockstep();
@@ -378,26 +385,9 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             const uint32_t lim = matchlimit - p;
             uint32_t ml = 0, bk = kNoBk;
             {
-                const uint32_t em1 = img.ld32(clampq(c0 - 4));
-                uint32_t ev[kFwdW];
-#pragma unroll
-                for (uint32_t i = 0; i < kFwdW; ++i) ev[i] = img.ld32(clampq(c0 + 4 * i));
                 const bool dist_ok = (TT == kByU16) || (c0 + kMaxDistance >= p);
                 if (valid && dist_ok) ml = fwd_match(dv, ev, lim);
                 if (p >= 4 && c0 >= 4) bk = back4(dm1, em1);
-            }
-            uint32_t pl = kNoBk, mlp = 0;
-            if (clash) {
-                // against the previous member of the group (bytes via ds_bpermute)
-                const uint64_t below = same & lanes_below;
-                const uint32_t src = below ? 63 - (uint32_t)__builtin_clzll(below) : lane;
-                uint32_t fv[kFwdW];
-#pragma unroll
-                for (uint32_t i = 0; i < kFwdW; ++i) fv[i] = shfl(dv[i], src);
-                if (below) {
-                    pl = src;
-                    if (valid) mlp = fwd_match(dv, fv, lim);
-                }
             }
             const uint64_t hitm = ballot(ml != 0);
             uint64_t put = 0;
@@ -464,6 +454,10 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             // is involved; recomputed per chain otherwise (see the walk).
             uint32_t fc0 = kStop, fe0 = 0, jv0 = lane;
             if (!limited) chain_tables(c0, ml, bk, fc0, fe0, jv0);
+            // the next window starts at or a little after B + 64: touch
+            // [B + 64, B + 320) now, one dword per lane, so that its loads hit
+            // cache (the value is only kept alive, never used)
+            pf = img.ld32(clampq(B + 64 + 4 * lane));
             if (kStamps) { st.cnt[0]++; st.lap(kPhSearch); }
 
             // ================= walk =========================================
@@ -596,12 +590,8 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                         } else {
                             const uint32_t cl = 63 - (uint32_t)__builtin_clzll(pm);
                             c = B + cl;
-                            if (cl == lane_val(pl, k)) {
-                                m = lane_val(mlp, k);
-                            } else {
-                                uint32_t bb;
-                                lanes_match(k, cl, m, bb);
-                            }
+                            uint32_t bb;
+                            lanes_match(k, cl, m, bb);
                         }
                     } else {
                         c = lane_val(c0, k);

@@ -44,6 +44,9 @@ LZ4E_DEV uint32_t put_lane(uint32_t v, uint32_t x, uint32_t l) {
 LZ4E_DEV uint32_t push_lane(uint32_t v, uint32_t dst) {
     return (uint32_t)__builtin_amdgcn_ds_permute((int)(dst << 2), (int)v);
 }
+// Keeps a value (e.g. a prefetch load's result) alive until here without
+// using it: the wait for it is placed here, not at the load.
+LZ4E_DEV void consume(uint32_t v) { asm volatile("" ::"v"(v)); }
 // ds_bpermute: lane src's value, per lane.
 LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return __shfl(v, (int)src); }
 LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) { return __shfl_up(v, d); }

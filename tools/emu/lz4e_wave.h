@@ -60,6 +60,7 @@ LZ4E_DEV uint32_t push_lane(uint32_t v, uint32_t dst) {
     g_wave->bar.arrive_and_wait();
     return r;
 }
+LZ4E_DEV void consume(uint32_t) {}
 LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)emu_gather(v, src); }
 LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) {
     g_wave->slot[g_lane] = (uint32_t)v;
