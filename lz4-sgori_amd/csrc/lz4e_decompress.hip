@@ -56,9 +56,12 @@ constexpr uint32_t kRing = 1024;                    // 4 segments of 256 B
 constexpr uint32_t kRingPad = 128;                  // mirror of ring bytes [0, 128)
 constexpr uint32_t kSink = 4 * kWave;               // a dword per lane for unwanted stores
 constexpr uint32_t kSpan = 64 * 32 + 16 + 48;       // a fast batch's output, 16-B aligned start
+constexpr uint32_t kJump = 2 * kSpan;               // u16 per span byte (chain resolution)
+constexpr uint16_t kFinal = 0xFFFF;                 // jump entry of a byte whose value is final
 
 typedef __attribute__((address_space(3))) uint8_t lu8;
 typedef __attribute__((address_space(3))) uint32_t lu32;
+typedef __attribute__((address_space(3))) uint16_t lu16;
 typedef uint32_t __attribute__((aligned(1))) u32a1;
 typedef __attribute__((address_space(3))) u32a1 lu32a1;
 
@@ -361,25 +364,45 @@ LZ4E_DEV void lane_zero(lu8* dst, int32_t len, lu8* sink) {
         put16(dst + t, make_uint4(0, 0, 0, 0), (uint32_t)(len - t < 16 ? len - t : 16), sink);
 }
 
-// The matches of lanes in `pending`, in lane order, each copied by the whole
-// wave: out[x] = out[x - off] for the match's bytes, min(off, 64) bytes per
-// step so that every source byte is final when read (offset 0 writes zeros).
-// Span index of position x: x - a0.
-LZ4E_DEV void serial_matches(lu8* span, int32_t a0, uint64_t pending, int32_t ms, int32_t m,
-                             int32_t off, uint32_t lane) {
-    while (pending) {
-        const uint32_t q = ctz64(pending);
-        pending &= pending - 1;
-        const int32_t qms = (int32_t)lane_val((uint32_t)ms, q) - a0;
-        const int32_t qm = (int32_t)lane_val((uint32_t)m, q);
-        const int32_t qoff = (int32_t)lane_val((uint32_t)off, q);
-        int32_t step = qoff == 0 || qoff > (int32_t)kWave ? (int32_t)kWave : qoff;
-        for (int32_t t0 = 0; t0 < qm; t0 += step) {
-            const int32_t t = t0 + (int32_t)lane;
-            if ((int32_t)lane < step && t < qm)
-                span[qms + t] = qoff ? span[qms - qoff + t] : (uint8_t)0;
+// Chains of dependent matches (a match whose source is the output of an
+// earlier, still pending one) by pointer jumping over span bytes: every byte
+// of a pending match points at the byte it copies (x - off), every other byte
+// of [lo_i, hi_i) is final; each whole-wave round either copies a byte whose
+// target is final or jumps it to its target's target, so a chain of depth d
+// takes about log2(d) rounds.  Targets lie at or after lo_i (the parts before
+// the batch were copied from HBM first).  Returns the number of rounds.
+LZ4E_DEV uint32_t resolve_chains(lu8* span, lu16* jump, int32_t lo_i, int32_t hi_i, int32_t s0,
+                                 bool mine, int32_t ms, int32_t m, int32_t off, uint32_t lane) {
+    for (int32_t i = lo_i + (int32_t)lane; i < hi_i; i += kWave) jump[i] = kFinal;
+    wave_fence();
+    if (mine) {
+        for (int32_t t = 0; t < m; ++t) {
+            if (off != 0) jump[ms + t] = (uint16_t)(ms + t - off);
+            else span[ms + t] = 0;  // offset 0: zeros, final
         }
     }
+    wave_fence();
+    uint32_t rounds = 0;
+    for (;;) {
+        bool more = false;
+        for (int32_t i = s0 + (int32_t)lane; i < hi_i; i += kWave) {
+            const uint32_t y = jump[i];
+            if (y != kFinal) {
+                const uint32_t z = jump[y];
+                if (z == kFinal) {
+                    span[i] = span[y];
+                    jump[i] = kFinal;
+                } else {
+                    jump[i] = (uint16_t)z;
+                    more = true;
+                }
+            }
+        }
+        wave_fence();
+        rounds++;
+        if (!ballot(more)) break;
+    }
+    return rounds;
 }
 
 // Per-lane copy of len bytes, non-overlapping, in 16-byte pieces.
@@ -455,7 +478,7 @@ struct Stamps {
 template <bool kStamps>
 LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, int32_t outSize,
                            int32_t* ret_slot, uint64_t* dbg, uint32_t lane, lu8* span,
-                           lu32* ring) {
+                           lu32* ring, lu16* jump) {
     Stamps st;
     auto lap = [&](int ph) {
         if constexpr (kStamps) {
@@ -678,12 +701,14 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
                 const int32_t mx = wave_excl_max(mine ? me : INT32_MIN);
                 const bool ready = mine && (need <= mn || ss2 >= mx);
                 const uint64_t rm = ballot(ready);
-                if (rm == (pending & (0 - pending)) && (pending & (pending - 1))) {
-                    // A dependency chain (only the first pending match is
-                    // ready): copy the pending matches one after another in
-                    // lane order, each by the whole wave (lane t: byte t).
-                    serial_matches(span, a0, pending, ms2, m2, r_off, lane);
-                    if constexpr (kStamps) st.rounds += popc64(pending);
+                const uint32_t np = popc64(pending);
+                if ((rm == (pending & (0 - pending)) && np > 1) || (np >= 4 && 4 * popc64(rm) <= np)) {
+                    // Dependency chains (few of the pending matches are
+                    // ready): resolve every pending byte by pointer jumping.
+                    const int32_t s0 = (int32_t)lane_val((uint32_t)ms2, ctz64(pending)) - a0;
+                    const uint32_t nr = resolve_chains(span, jump, lo - a0, op - a0, s0, mine,
+                                                       ms2 - a0, m2, r_off, lane);
+                    if constexpr (kStamps) st.rounds += nr;
                     pending = 0;
                     break;
                 }
@@ -816,9 +841,10 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
     uint64_t* d = kStamps && dbg ? dbg + 8 * (size_t)b : nullptr;
     if (special_case(in, srcSize, outSize, ret + b, lane)) return;
     // LDS: [input ring + mirror] [store sink] [span]
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kRing + kRingPad + kSink + kSpan];
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kRing + kRingPad + kSink + kSpan + kJump];
     decode_block<kStamps>(in, srcSize, out, outSize, ret + b, d, lane,
-                          (lu8*)(smem + kRing + kRingPad + kSink), (lu32*)smem);
+                          (lu8*)(smem + kRing + kRingPad + kSink), (lu32*)smem,
+                          (lu16*)(smem + kRing + kRingPad + kSink + kSpan));
 }
 
 template <bool kStamps>
