@@ -81,7 +81,13 @@ struct Table {
 struct HbmImage {
     gcu8* p;
     uint32_t n;
+    ByteBuf buf;  // the same bytes as a buffer resource (window loads)
     LZ4E_DEV uint32_t rd8(uint32_t q) const { return p[q]; }
+    // Window loads: dword at q, 0 when any of its bytes lies outside the
+    // block (callers never use such a dword: every compared byte is in one
+    // fully inside); buffer loads take the constant part of the offset in
+    // the instruction and merge into dwordx4.
+    LZ4E_DEV uint32_t wld(uint32_t q) const { return buf_ld32(buf, q); }
     LZ4E_DEV uint32_t ld32(uint32_t q) const { return *(gcu32*)(p + vaddr(q)); }
     LZ4E_DEV uint64_t ld64(uint32_t q) const { return *(gcu64*)(p + vaddr(q)); }
     // Lanes past the block (or before it, X < 4) read a clamped, meaningless
@@ -109,6 +115,7 @@ struct LdsImage {
                alignbyte(w1, w0, r);
     }
     LZ4E_DEV uint32_t stripe(uint32_t X, uint32_t lane) const { return ld32(X - 4 + 4 * lane); }
+    LZ4E_DEV uint32_t wld(uint32_t q) const { return ld32(q); }
 };
 
 // Phase cycle counters of the diagnostic build (launch_compress_stamped).
@@ -310,7 +317,6 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
         const uint32_t mflimit = n - kMfLimit;
         const uint32_t matchlimit = n - kLastLiterals;
         const uint64_t lanes_below = (1ull << lane) - 1;
-        auto clampq = [&](uint32_t q) { return q < n - 4 ? q : n - 4; };
 
         // ---- sequence output -------------------------------------------
         // offset, match-length code and token of a sequence whose token slot
@@ -352,20 +358,20 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             const uint32_t B = rmode ? e - 2 : e;
             const uint32_t p = B + lane;
             const bool valid = p <= mflimit;  // every put / lookup is at <= mflimit
-            const uint32_t dm1 = img.ld32(clampq(p - 4));
+            const uint32_t dm1 = img.wld(p - 4);
             uint32_t dv[kFwdW];  // bytes p .. p + kFwd - 1
 #pragma unroll
-            for (uint32_t i = 0; i < kFwdW; ++i) dv[i] = img.ld32(clampq(p + 4 * i));
+            for (uint32_t i = 0; i < kFwdW; ++i) dv[i] = img.wld(p + 4 * i);
             const uint32_t d0 = dv[0];
             const uint32_t h = hash_val<TT>(((uint64_t)dv[1] << 32) | d0);
             uint32_t c0 = 0, rb = p;
             lockstep();  // the previous window's commit is in the table
             if (valid) c0 = T.get(h);  // snapshot
             // the snapshot candidate's bytes: issued now, used after the clash groups
-            const uint32_t em1 = img.ld32(clampq(c0 - 4));
+            const uint32_t em1 = img.wld(c0 - 4);
             uint32_t ev[kFwdW];
 #pragma unroll
-            for (uint32_t i = 0; i < kFwdW; ++i) ev[i] = img.ld32(clampq(c0 + 4 * i));
+            for (uint32_t i = 0; i < kFwdW; ++i) ev[i] = img.wld(c0 + 4 * i);
             lockstep();
             if (valid) T.put(h, p);  // speculative put of every position
             lockstep();
@@ -457,7 +463,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             // the next window starts at or a little after B + 64: touch
             // [B + 64, B + 320) now, one dword per lane, so that its loads hit
             // cache (the value is only kept alive, never used)
-            pf = img.ld32(clampq(B + 64 + 4 * lane));
+            pf = img.wld(B + 64 + 4 * lane);
             if (kStamps) { st.cnt[0]++; st.lap(kPhSearch); }
 
             // ================= walk =========================================
@@ -979,7 +985,7 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
         dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane);
     } else {
         block_sync();
-        const HbmImage img{(gcu8*)in, n};
+        const HbmImage img{(gcu8*)in, n, buf_make(in, n)};
         dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane);
     }
 }

@@ -123,6 +123,19 @@ LZ4E_DEV uint32_t vaddr(uint32_t q) {
 // their address space and would otherwise compile to flat_* accesses, which
 // also count on lgkmcnt (coupling them to every LDS wait).
 typedef __attribute__((address_space(1))) const uint32_t gcu32;
+
+// n bytes at p as a raw buffer resource: dword loads at byte offset q return
+// 0 when the dword is not entirely inside [0, n) (hardware range check).
+struct ByteBuf {
+    __amdgpu_buffer_rsrc_t r;
+};
+LZ4E_DEV ByteBuf buf_make(const void* p, uint32_t n) {
+    return ByteBuf{__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)n,
+                                                     0x00020000)};
+}
+LZ4E_DEV uint32_t buf_ld32(const ByteBuf& b, uint32_t q) {
+    return __builtin_amdgcn_raw_buffer_load_b32(b.r, q, 0, 0);
+}
 typedef __attribute__((address_space(1))) const uint8_t gcu8;
 
 }  // namespace lz4e

@@ -105,4 +105,16 @@ LZ4E_DEV uint32_t vaddr(uint32_t q) { return q; }
 typedef const uint32_t gcu32;
 typedef const uint8_t gcu8;
 
+struct ByteBuf {
+    const uint8_t* p;
+    uint32_t n;
+};
+inline ByteBuf buf_make(const void* p, uint32_t n) { return ByteBuf{(const uint8_t*)p, n}; }
+inline uint32_t buf_ld32(const ByteBuf& b, uint32_t q) {
+    if ((uint64_t)q + 4 > b.n) return 0;
+    uint32_t v;
+    __builtin_memcpy(&v, b.p + q, 4);
+    return v;
+}
+
 }  // namespace lz4e
