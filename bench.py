@@ -18,7 +18,8 @@ configurations: fio4k (configs[2]), sg512 (configs[3], byU32), text256k
 
 Multi-GPU (torch.distributed.run, one rank per GPU): blocks are independent,
 each rank owns its own shard (weak scaling, no data-path collective); the
-only collective is the max-over-ranks reduction of the timing.
+only collectives (lz4e_amd.shards) are the frame-stream layout all_gather and
+the max-over-ranks reduction of the timing.
 """
 import argparse
 import json
@@ -34,6 +35,7 @@ sys.path.insert(0, os.path.join(REPO, "lz4-sgori_amd"))
 
 import lz4e_amd  # noqa: E402
 from lz4e_amd import BYU16, BYU32, corpus  # noqa: E402
+from lz4e_amd.shards import frame_layout, reduce_step  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -159,16 +161,10 @@ def main():
     comp_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
     step_s = elapsed / args.steps
-    if dist:
-        v = torch.tensor([step_s, comp_ms, dec_ms, float(C)], dtype=torch.float64, device=dev)
-        mx = v.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = v.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        step_s, comp_ms, dec_ms = float(mx[0]), float(mx[1]), float(mx[2])
-        C_all = float(sm[3])
-    else:
-        C_all = float(C)
+    group = dist.group.WORLD if dist else None
+    # this rank's place in the job's frame stream (all_gather + exclusive scan)
+    _, C_all, _ = frame_layout(C, nblk, group, dev)
+    (step_s, comp_ms, dec_ms), _ = reduce_step([step_s, comp_ms, dec_ms], C, group, dev)
     U_all = U * world
     value = U_all / step_s / 2**30
 

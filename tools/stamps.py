@@ -65,7 +65,7 @@ def run(name, data, bs, cls, label):
           f"cycles/seq {tot.sum() / max(1, seqs.sum()):.0f}; fast attempts {fa.mean():.0f} fast seqs {fev.mean():.0f}")
     for i, p in enumerate(ph):
         print(f"   {p:8s} {d[:, i].mean():12.0f}  ({100 * d[:, i].sum() / tot.sum():5.1f}%)")
-    by_class(name, tot, n, lambda m: f"seq {seqs[m].mean():.0f} srch {srch[m].mean():.0f} " + " ".join(f"{ph[i]}={d[m, i].mean():.0f}" for i in range(6)))
+    by_class(name, tot, n, lambda m: f"seq {seqs[m].mean():.0f} win {srch[m].mean():.0f} pass {rem[m].mean():.0f} att {fa[m].mean():.0f} fseq {fev[m].mean():.0f} " + " ".join(f"{ph[i]}={d[m, i].mean():.0f}" for i in range(6)))
 
 if __name__ == "__main__":
     mode = os.environ.get("LZ4E_COMPRESS_LDS_MAX", "default")
