@@ -256,13 +256,23 @@ constexpr uint32_t kNoBk = 0xFF;   // bk: backward bytes not available in regist
 // Forward match of the kFwd bytes a[] against b[], lane-wise: 0 if the first
 // 4 bytes differ, the matched length capped at lim, or kFwd | kLong.
 LZ4E_DEV uint32_t fwd_match(const uint32_t* a, const uint32_t* b, uint32_t lim) {
-    if (a[0] != b[0]) return 0;
-    uint32_t m = kFwd;
+    // first mismatching dword among 1..3, then (only if those are all equal)
+    // among 4..7 -- most matches end in the first 16 bytes
+    uint32_t m = 16;
 #pragma unroll
-    for (int i = (int)kFwdW - 1; i >= 1; --i) {
+    for (int i = 3; i >= 1; --i) {
         const uint32_t x = a[i] ^ b[i];
         if (x) m = 4 * (uint32_t)i + ((uint32_t)__builtin_ctz(x) >> 3);
     }
+    if (m == 16) {
+        m = kFwd;
+#pragma unroll
+        for (int i = (int)kFwdW - 1; i >= 4; --i) {
+            const uint32_t x = a[i] ^ b[i];
+            if (x) m = 4 * (uint32_t)i + ((uint32_t)__builtin_ctz(x) >> 3);
+        }
+    }
+    if (a[0] != b[0]) return 0;
     if (m >= lim) return lim;
     return m == kFwd ? (kFwd | kLong) : m;
 }
@@ -459,7 +469,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             // Tables for the snapshot candidates: exact wherever no clash lane
             // is involved; recomputed per chain otherwise (see the walk).
             uint32_t fc0 = kStop, fe0 = 0, jv0 = lane;
-            if (!limited) chain_tables(c0, ml, bk, fc0, fe0, jv0);
+            bool have0 = false;  // snapshot tables built (on first use)
             // the next window starts at or a little after B + 64: touch
             // [B + 64, B + 320) now, one dword per lane, so that its loads hit
             // cache (the value is only kept alive, never used)
@@ -481,9 +491,18 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                     const uint32_t ks = e - B;
                     uint32_t k = ks, nev = 0, ev = 0;
                     uint64_t evm = 0, pch = 0;
-                    uint32_t fc = fc0, fe = fe0, jv = jv0;
+                    uint32_t fc = kStop, fe = 0, jv = lane;
                     if (ks < 64) {
                         const bool dyn = (clash >> ks) != 0;
+                        if (!dyn) {
+                            if (!have0) {
+                                chain_tables(c0, ml, bk, fc0, fe0, jv0);
+                                have0 = true;
+                            }
+                            fc = fc0;
+                            fe = fe0;
+                            jv = jv0;
+                        }
                         uint64_t Pg = put | (1ull << (ks - 2)) | lane_range(ks, 63);
                         constexpr uint32_t kMaxPass = 6;
                         for (uint32_t pass = 0;; ++pass) {
