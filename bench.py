@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--cpu-blocks", type=int, default=0, help="CPU baseline sample size in blocks")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the PCIe-inclusive chunk-layer run")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -72,6 +73,46 @@ def make_data(gen: str, nbytes: int, seed: int) -> np.ndarray:
     if gen == "fio":
         return corpus.fio_pattern(nbytes, seed)
     return corpus.text_proxy(nbytes, seed)
+
+
+def end_to_end(host: np.ndarray, nblk: int, bs: int, cls: int, reps: int = 3) -> dict:
+    """lz4e_chunk_write_batch over the same blocks given as host bio_vec lists
+    (16 x 4 KiB segments per 64 KiB block, 128 x 512 B for sg512): SG gather
+    -> H2D -> compress -> decompress -> D2H -> copy-out, two pipeline slots.
+    The host buffers are pageable numpy memory, as a bio's pages would be."""
+    import ctypes
+    seg = 512 if cls == BYU32 and bs == 65536 else min(bs, 4096)
+    nseg = bs // seg
+    base = host.ctypes.data
+    bv = (lz4e_amd.BioVec * (nblk * nseg))()
+    addr = np.frombuffer(bv, dtype=np.dtype([("p", "<u8"), ("l", "<u4"), ("o", "<u4")]))
+    addr["p"] = base + np.arange(nblk * nseg, dtype=np.uint64) * seg
+    addr["l"] = seg
+    addr["o"] = 0
+    its = (lz4e_amd.BvecIter * nblk)()
+    out = np.empty(nblk * bs, np.uint8)
+    reqs = (lz4e_amd.ChunkRequest * nblk)()
+    bvp = ctypes.cast(bv, ctypes.c_void_p).value
+    for i in range(nblk):
+        its[i].bi_size = bs
+        reqs[i].src = ctypes.cast(bvp + i * nseg * ctypes.sizeof(lz4e_amd.BioVec),
+                                  ctypes.POINTER(lz4e_amd.BioVec))
+        reqs[i].srcIter = ctypes.pointer(its[i])
+        reqs[i].data = out.ctypes.data + i * bs
+    L = lz4e_amd.lib()
+    times = []
+    for r in range(reps + 1):
+        t0 = time.perf_counter()
+        good = L.lz4e_chunk_write_batch(reqs, nblk, None)
+        times.append(time.perf_counter() - t0)
+        if good != nblk:
+            raise SystemExit(f"bench: chunk pipeline failed ({good}/{nblk}): {lz4e_amd.last_error()}")
+    if not np.array_equal(out, host[:nblk * bs]):
+        raise SystemExit("bench: chunk pipeline round trip mismatch")
+    t = float(np.median(times[1:]))
+    return {"value": round(nblk * bs / t / 2**30, 3), "unit": "GiB/s", "ms": round(t * 1e3, 2),
+            "path": f"lz4e_chunk_write_batch: {nblk} WRITE bios of {nseg} x {seg} B host segments, "
+                    "SG gather -> H2D -> compress -> decompress -> D2H -> copy-out (PCIe-inclusive)"}
 
 
 def main():
@@ -197,6 +238,10 @@ def main():
         "decompress_GiBps": round(U_all / (dec_ms / 1e3) / 2**30, 3),
         "roofline": roofline,
     }
+
+    # ---- end to end through the chunk layer (PCIe-inclusive, never `value`) ----
+    if not args.no_e2e:
+        result["end_to_end"] = end_to_end(host, nblk, bs, cls)
 
     # ---- CPU baseline (rank 0, N=1 only) ---------------------------------------
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -203,6 +203,46 @@ int lz4e_decompress_batch_dev(const uint8_t *src, const uint64_t *src_off,
 			      const uint64_t *dst_off, const int32_t *dst_cap,
 			      int32_t *ret, uint32_t nblocks, void *stream);
 
+/*
+ * Chunk-layer WRITE round trip, batched and streamed.
+ * Per request this is the data path of lz4e_write_req_init
+ * (lz4e_bdev/lz4e_req.c:144-213): lz4e_chunk_compress_ext
+ * (lz4e_bdev/lz4e_chunk.c:139-159: LZ4E_compress_default of the bio's SG
+ * payload into a LZ4E_COMPRESSBOUND-sized chunk, i.e. never output-limited),
+ * then lz4e_chunk_decompress (lz4e_chunk.c:119-137: LZ4_decompress_safe of
+ * that frame back into the chunk's contiguous source buffer, whose size must
+ * equal the bio's, lz4e_chunk.c:133).  Requests flow through two pipeline
+ * slots (pinned staging + HBM buffers + a HIP stream each): the SG gather of
+ * one sub-batch overlaps the H2D copy, both kernels and the D2H copy of the
+ * other.
+ */
+struct lz4e_chunk_request {
+	const struct bio_vec *src;       /* original bio's bi_io_vec            */
+	const struct bvec_iter *srcIter; /* original bio's bi_iter (read only:
+					    the chunk layer passes a copy)      */
+	char *data;        /* src_buf.data: receives srcIter->bi_size bytes    */
+	char *frame;       /* nullable: receives the frame (dst_buf.data)      */
+	int frame_cap;     /* bytes available at frame                         */
+	int comp_size;     /* out: dst_buf.data_size (0 on compress failure)   */
+	int status;        /* out: 0, -EIO (-5) like the chunk layer, or
+			      -ENOSPC (-28) when frame_cap < comp_size          */
+};
+
+/* Counters of one call, in the spirit of lz4e_bdev/lz4e_stats.c:39-52
+ * (reqs_total / reqs_failed / data_in_bytes of the requests handled here;
+ * frame_bytes = sum of comp_size). */
+struct lz4e_chunk_stats {
+	uint64_t reqs_total;
+	uint64_t reqs_failed;
+	uint64_t data_in_bytes;
+	uint64_t frame_bytes;
+};
+
+/* Returns the number of requests with status 0, or -1 when no GPU is usable
+ * (every status is then -EIO).  `stats` is nullable; it is added to. */
+int lz4e_chunk_write_batch(struct lz4e_chunk_request *reqs, int n,
+			   struct lz4e_chunk_stats *stats);
+
 #ifdef __cplusplus
 }
 #endif

@@ -389,13 +389,12 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             const uint64_t cm = ballot(rb != p);
             uint64_t same = 0;  // valid lanes sharing my hash (clash groups only)
             if (cm) {
-                uint64_t todo = cm;
-                do {
-                    const uint32_t hg = lane_val(h, ctz64(todo));
-                    const uint64_t m = ballot(valid && h == hg);
-                    if (h == hg) same = m;
-                    todo &= ~m;
-                } while (todo);
+                // A valid lane reads back the position of its group's winning
+                // put, so rb - B names the group (invalid lanes: none; their
+                // `same` only steers the walk between two exact table builds).
+                const uint64_t vmask = ballot(valid);
+                const uint64_t m = match_any6(rb - B) & vmask;
+                if (valid && (m & (m - 1))) same = m;
             }
             const uint64_t clash = ballot(same != 0);
             const uint32_t lim = matchlimit - p;

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lz4e.h"
@@ -444,6 +445,262 @@ int lz4e_decompress_batch_dev(const uint8_t* src, const uint64_t* src_off, const
     return hip_ok(lz4e::launch_decompress(a, static_cast<hipStream_t>(stream)), "decompress launch")
                ? 0
                : -1;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Chunk-layer write round trip (include/lz4e.h lz4e_chunk_write_batch)
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr int kEIO = -5, kENOSPC = -28;
+constexpr uint64_t kSubBytes = 32ull << 20;  // input bytes per pipeline sub-batch
+constexpr uint32_t kSubReqs = 16384;         // requests per sub-batch
+
+// Runs f(j) for j in [0, n) on up to 8 host threads when the bytes justify it.
+template <class F>
+void par_for(uint32_t n, uint64_t bytes, F f) {
+    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const uint32_t T = bytes < (4ull << 20) ? 1u : std::min({8u, hw, n});
+    if (T <= 1) {
+        for (uint32_t j = 0; j < n; ++j) f(j);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            for (uint32_t j = t; j < n; j += T) f(j);
+        });
+    for (auto& x : th) x.join();
+}
+
+// Per-sub-batch metadata (device + pinned host), one entry per request.
+struct ChunkMeta {
+    size_t in_off, in_len, ttype, fr_off, fr_cap, out_off, out_cap, ret, dret, total;
+    explicit ChunkMeta(uint32_t R) {
+        size_t o = 0;
+        in_off = o;  o += align16(8ull * R);
+        in_len = o;  o += align16(4ull * R);
+        ttype = o;   o += align16(1ull * R);
+        fr_off = o;  o += align16(8ull * R);
+        fr_cap = o;  o += align16(4ull * R);
+        out_off = o; o += align16(8ull * R);
+        out_cap = o; o += align16(4ull * R);
+        ret = o;     o += align16(4ull * R);
+        dret = o;    o += align16(4ull * R);
+        total = o;
+    }
+};
+
+struct ChunkSlot {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    HostBuf h_data, h_meta;
+    DevBuf d_data, d_meta;
+    bool busy = false;
+    bool want_frames = false;
+    std::vector<uint32_t> req;        // request index per entry
+    std::vector<uint64_t> fr, out;    // frame / output offsets in the data buffer
+    uint64_t in_bytes = 0, fr_bytes = 0, out_bytes = 0;
+    size_t meta_ret = 0, meta_dret = 0;
+};
+
+struct ChunkCtx {
+    std::mutex mu;
+    ChunkSlot slot[2];
+    bool ready = false;
+    bool init() {
+        if (ready) return true;
+        for (auto& s : slot)
+            if (!hip_ok(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate") ||
+                !hip_ok(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate"))
+                return false;
+        ready = true;
+        return true;
+    }
+};
+
+ChunkCtx& chunk_ctx() {
+    static ChunkCtx c;
+    return c;
+}
+
+// Waits for a slot's sub-batch and hands its results to the requests.
+bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chunk_stats* st,
+                  int& good) {
+    if (!s.busy) return true;
+    s.busy = false;
+    if (!hip_ok(hipEventSynchronize(s.done), "chunk sync")) return false;
+    const uint8_t* hd = static_cast<const uint8_t*>(s.h_data.p);
+    const uint8_t* hm = static_cast<const uint8_t*>(s.h_meta.p);
+    const int32_t* ret = reinterpret_cast<const int32_t*>(hm + s.meta_ret);
+    const int32_t* dret = reinterpret_cast<const int32_t*>(hm + s.meta_dret);
+    const uint32_t R = (uint32_t)s.req.size();
+    par_for(R, s.out_bytes, [&](uint32_t j) {
+        lz4e_chunk_request& q = reqs[s.req[j]];
+        const int32_t len = (int32_t)q.srcIter->bi_size;
+        q.comp_size = ret[j] > 0 ? ret[j] : 0;
+        if (ret[j] <= 0 || dret[j] != len) {  // lz4e_chunk.c:110-113, 127-133
+            q.status = kEIO;
+            return;
+        }
+        if (q.frame) {
+            if (q.frame_cap < ret[j]) {
+                q.status = kENOSPC;
+                return;
+            }
+            std::memcpy(q.frame, hd + s.fr[j], (size_t)ret[j]);
+        }
+        if (len > 0) std::memcpy(q.data, hd + s.out[j], (size_t)len);
+        q.status = 0;
+    });
+    for (uint32_t j = 0; j < R; ++j) {
+        const lz4e_chunk_request& q = reqs[s.req[j]];
+        if (q.status == 0) good++;
+        if (st) {
+            st->reqs_total++;
+            if (q.status != 0) st->reqs_failed++;
+            else st->data_in_bytes += q.srcIter->bi_size;
+            st->frame_bytes += (uint64_t)q.comp_size;
+        }
+    }
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_chunk_stats* stats) {
+    if (n <= 0) return 0;
+    for (int i = 0; i < n; ++i) {
+        reqs[i].comp_size = 0;
+        reqs[i].status = kEIO;
+    }
+    Ctx& c = ctx();
+    {
+        std::lock_guard<std::mutex> lk(c.mu);
+        g_err.clear();
+        if (!c.init()) return -1;
+    }
+    ChunkCtx& cc = chunk_ctx();
+    std::lock_guard<std::mutex> lk(cc.mu);
+    if (!cc.init()) return -1;
+
+    int good = 0;
+    uint32_t i = 0, k = 0;
+    const uint32_t N = (uint32_t)n;
+    while (i < N) {
+        ChunkSlot& s = cc.slot[k & 1];
+        if (!chunk_finish(s, reqs, stats, good)) return -1;
+        // ---- form the sub-batch: requests [i, e) ----
+        s.req.clear();
+        s.fr.clear();
+        s.out.clear();
+        std::vector<uint64_t> in;
+        std::vector<uint8_t> tt;
+        uint64_t ib = 0, fb = 0, ob = 0;
+        uint32_t max_len = 0;
+        bool frames = false;
+        for (; i < N && s.req.size() < kSubReqs && (s.req.empty() || ib < kSubBytes); ++i) {
+            const lz4e_chunk_request& q = reqs[i];
+            const uint32_t len = q.srcIter->bi_size;
+            int t = LZ4E_TABLE_BYU16;
+            if (len > LZ4E_MAX_INPUT_SIZE) {  // lz4e_compress.c:245-248 -> -EIO
+                if (stats) stats->reqs_total++, stats->reqs_failed++;
+                continue;
+            }
+            if (len >= 13 && (t = table_type_of(q.src, q.srcIter)) == 0) {  // :274-277
+                if (stats) stats->reqs_total++, stats->reqs_failed++;
+                continue;
+            }
+            s.req.push_back(i);
+            in.push_back(ib);
+            tt.push_back((uint8_t)t);
+            ib += align16(len);
+            s.fr.push_back(fb);
+            fb += align16((uint64_t)bound_of(len) + 64);
+            s.out.push_back(ob);
+            ob += align16((uint64_t)len + 64);
+            max_len = std::max(max_len, len);
+            frames |= q.frame != nullptr;
+        }
+        const uint32_t R = (uint32_t)s.req.size();
+        if (R == 0) continue;
+        for (uint32_t j = 0; j < R; ++j) {  // one data buffer: [inputs | frames | outputs]
+            s.fr[j] += ib;
+            s.out[j] += ib + fb;
+        }
+        s.in_bytes = ib;
+        s.fr_bytes = fb;
+        s.out_bytes = ob;
+        s.want_frames = frames;
+        const ChunkMeta m(R);
+        const uint64_t total = ib + fb + ob;
+        if (!s.h_data.ensure(total) || !s.d_data.ensure(total) || !s.h_meta.ensure(m.total) ||
+            !s.d_meta.ensure(m.total))
+            return -1;
+        uint8_t* hd = static_cast<uint8_t*>(s.h_data.p);
+        uint8_t* hm = static_cast<uint8_t*>(s.h_meta.p);
+        // ---- gather (overlaps the other slot's GPU work) ----
+        par_for(R, ib, [&](uint32_t j) {
+            const lz4e_chunk_request& q = reqs[s.req[j]];
+            sg_gather(q.src, *q.srcIter, hd + in[j], q.srcIter->bi_size);
+        });
+        for (uint32_t j = 0; j < R; ++j) {
+            const uint32_t len = reqs[s.req[j]].srcIter->bi_size;
+            reinterpret_cast<uint64_t*>(hm + m.in_off)[j] = in[j];
+            reinterpret_cast<uint32_t*>(hm + m.in_len)[j] = len;
+            (hm + m.ttype)[j] = tt[j];
+            reinterpret_cast<uint64_t*>(hm + m.fr_off)[j] = s.fr[j];
+            reinterpret_cast<uint32_t*>(hm + m.fr_cap)[j] = bound_of(len);  // dst_buf.buf_size
+            reinterpret_cast<uint64_t*>(hm + m.out_off)[j] = s.out[j];
+            reinterpret_cast<int32_t*>(hm + m.out_cap)[j] = (int32_t)len;  // src_buf.buf_size
+        }
+        s.meta_ret = m.ret;
+        s.meta_dret = m.dret;
+        uint8_t* dd = static_cast<uint8_t*>(s.d_data.p);
+        uint8_t* dm = static_cast<uint8_t*>(s.d_meta.p);
+        if (!hip_ok(hipMemcpyAsync(dd, hd, ib, hipMemcpyHostToDevice, s.stream), "H2D data") ||
+            !hip_ok(hipMemcpyAsync(dm, hm, m.ret, hipMemcpyHostToDevice, s.stream), "H2D meta"))
+            return -1;
+        const lz4e::CompressBatch ca{dd,
+                                     reinterpret_cast<const uint64_t*>(dm + m.in_off),
+                                     reinterpret_cast<const uint32_t*>(dm + m.in_len),
+                                     dm + m.ttype,
+                                     dd,
+                                     reinterpret_cast<const uint64_t*>(dm + m.fr_off),
+                                     reinterpret_cast<const uint32_t*>(dm + m.fr_cap),
+                                     reinterpret_cast<int32_t*>(dm + m.ret),
+                                     nullptr,
+                                     R,
+                                     max_len};
+        // the frame sizes feed the decoder straight from HBM (no host trip)
+        const lz4e::DecompressBatch da{dd,
+                                       reinterpret_cast<const uint64_t*>(dm + m.fr_off),
+                                       reinterpret_cast<const int32_t*>(dm + m.ret),
+                                       dd,
+                                       reinterpret_cast<const uint64_t*>(dm + m.out_off),
+                                       reinterpret_cast<const int32_t*>(dm + m.out_cap),
+                                       reinterpret_cast<int32_t*>(dm + m.dret),
+                                       R};
+        if (!hip_ok(lz4e::launch_compress(ca, s.stream), "compress launch") ||
+            !hip_ok(lz4e::launch_decompress(da, s.stream), "decompress launch") ||
+            !hip_ok(hipMemcpyAsync(hm + m.ret, dm + m.ret, m.total - m.ret, hipMemcpyDeviceToHost,
+                                   s.stream), "D2H meta") ||
+            (frames && !hip_ok(hipMemcpyAsync(hd + ib, dd + ib, fb, hipMemcpyDeviceToHost, s.stream),
+                               "D2H frames")) ||
+            !hip_ok(hipMemcpyAsync(hd + ib + fb, dd + ib + fb, ob, hipMemcpyDeviceToHost, s.stream),
+                    "D2H data") ||
+            !hip_ok(hipEventRecord(s.done, s.stream), "event record"))
+            return -1;
+        s.busy = true;
+        k++;
+    }
+    for (uint32_t t = 0; t < 2; ++t)
+        if (!chunk_finish(cc.slot[(k + t) & 1], reqs, stats, good)) return -1;
+    return good;
 }
 
 }  // extern "C"

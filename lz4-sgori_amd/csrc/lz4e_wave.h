@@ -39,6 +39,18 @@ LZ4E_DEV uint32_t put_lane(uint32_t v, uint32_t x, uint32_t l) {
     return v;
 }
 #pragma clang diagnostic pop
+// Lanes whose 6-bit key equals mine (key < 64): one ballot per key bit, no
+// loop over the distinct keys.
+LZ4E_DEV uint64_t match_any6(uint32_t key) {
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (uint32_t b = 0; b < 6; ++b) {
+        const bool bit = (key >> b) & 1;
+        const uint64_t bb = ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
 // ds_permute: lane l sends v to lane dst (l's own choice); a lane nobody
 // sends to receives an unspecified value.
 LZ4E_DEV uint32_t push_lane(uint32_t v, uint32_t dst) {

@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "LZ4E_compress_default", "LZ4E_decompress_safe", "lz4e_sg_table_type",
     "lz4e_last_error", "lz4e_gpu_available", "lz4e_compress_sg_batch",
     "lz4e_decompress_batch", "lz4e_compress_batch_dev", "lz4e_decompress_batch_dev",
+    "lz4e_chunk_write_batch",
 )
 
 
@@ -76,6 +77,21 @@ class SgRequest(ctypes.Structure):
                 ("srcIter", ctypes.POINTER(BvecIter)), ("dstIter", ctypes.POINTER(BvecIter)),
                 ("ret", ctypes.c_int)]
 
+
+class ChunkRequest(ctypes.Structure):
+    """struct lz4e_chunk_request (include/lz4e.h)."""
+    _fields_ = [("src", ctypes.POINTER(BioVec)), ("srcIter", ctypes.POINTER(BvecIter)),
+                ("data", ctypes.c_void_p), ("frame", ctypes.c_void_p), ("frame_cap", ctypes.c_int),
+                ("comp_size", ctypes.c_int), ("status", ctypes.c_int)]
+
+
+class ChunkStats(ctypes.Structure):
+    """struct lz4e_chunk_stats (include/lz4e.h)."""
+    _fields_ = [("reqs_total", ctypes.c_uint64), ("reqs_failed", ctypes.c_uint64),
+                ("data_in_bytes", ctypes.c_uint64), ("frame_bytes", ctypes.c_uint64)]
+
+
+EIO, ENOSPC = 5, 28
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -117,6 +133,8 @@ def lib() -> ctypes.CDLL:
     L.lz4e_compress_batch_dev.restype = I32
     L.lz4e_decompress_batch_dev.argtypes = [P, P, P, P, P, P, P, U32, P]
     L.lz4e_decompress_batch_dev.restype = I32
+    L.lz4e_chunk_write_batch.argtypes = [ctypes.POINTER(ChunkRequest), I32, ctypes.POINTER(ChunkStats)]
+    L.lz4e_chunk_write_batch.restype = I32
     _lib = L
     return L
 
@@ -281,6 +299,38 @@ def decompress_batch(frames: Sequence[bytes], caps: Sequence[int]) -> List[Tuple
     if lib().lz4e_decompress_batch(sp, cs, dp, cp, rt, n) < 0:
         raise GpuUnavailable(last_error())
     return [(rt[i], dsts[i].raw[:max(rt[i], 0)]) for i in range(n)]
+
+
+def chunk_write_batch(srcs: Sequence[SgList], want_frames: bool = False,
+                      stats: Optional[ChunkStats] = None):
+    """lz4e_chunk_write_batch over WRITE bios given as SG lists.
+
+    Returns (good, [(status, comp_size, data bytes, frame bytes or None)]),
+    the chunk layer's result per request (lz4e_bdev/lz4e_req.c:144-213)."""
+    _require_gpu()
+    n = len(srcs)
+    reqs = (ChunkRequest * max(1, n))()
+    datas, frames = [], []
+    for i, s in enumerate(srcs):
+        size = s.it.bi_size
+        d = ctypes.create_string_buffer(max(1, size))
+        f = ctypes.create_string_buffer(max(1, compress_bound(size))) if want_frames else None
+        datas.append(d)
+        frames.append(f)
+        reqs[i].src = s.bvecs
+        reqs[i].srcIter = ctypes.pointer(s.it)
+        reqs[i].data = ctypes.addressof(d)
+        reqs[i].frame = ctypes.addressof(f) if f is not None else None
+        reqs[i].frame_cap = compress_bound(size) if f is not None else 0
+    good = lib().lz4e_chunk_write_batch(reqs, n, ctypes.byref(stats) if stats is not None else None)
+    if good < 0:
+        raise GpuUnavailable(last_error())
+    out = []
+    for i, s in enumerate(srcs):
+        r = reqs[i]
+        fr = frames[i].raw[:r.comp_size] if frames[i] is not None and r.status == 0 else None
+        out.append((r.status, r.comp_size, datas[i].raw[:s.it.bi_size] if r.status == 0 else None, fr))
+    return good, out
 
 
 # ---------------------------------------------------------------------------

@@ -94,3 +94,21 @@ def test_no_gpu_fails_loudly(amd):
     assert amd.lib().LZ4E_decompress_safe(b"\x10a", buf, 2, 64) < 0
     with pytest.raises(amd.GpuUnavailable):
         amd.compress_default(src, dst)
+
+
+def test_chunk_write_batch_no_gpu(amd):
+    """Without a GPU the chunk pipeline reports -1 and marks every request -EIO."""
+    if amd.gpu_available():
+        pytest.skip("a GPU is visible")
+    data = b"abcd" * 100
+    src = make_sg(data, [len(data)])
+    reqs = (lz4e_amd.ChunkRequest * 1)()
+    buf = ctypes.create_string_buffer(len(data))
+    reqs[0].src = src.bvecs
+    reqs[0].srcIter = ctypes.pointer(src.it)
+    reqs[0].data = ctypes.addressof(buf)
+    st = lz4e_amd.ChunkStats()
+    assert amd.lib().lz4e_chunk_write_batch(reqs, 1, ctypes.byref(st)) == -1
+    assert reqs[0].status == -lz4e_amd.EIO and reqs[0].comp_size == 0
+    with pytest.raises(amd.GpuUnavailable):
+        amd.chunk_write_batch([src])

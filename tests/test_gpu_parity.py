@@ -347,3 +347,68 @@ def test_decompress_periodic_matches(gpu, cap_extra):
     for i in range(len(frames)):
         assert r[i] == len(expect[i]), i
         assert outs[i] == expect[i], i
+
+
+# ---------------------------------------------------------------------------
+# chunk-layer write round trip (lz4e_bdev/lz4e_req.c:144-213)
+# ---------------------------------------------------------------------------
+
+def _chunk_check(gpu, srcs, payloads, want_frames=True):
+    stats = gpu.ChunkStats()
+    good, res = gpu.chunk_write_batch(srcs, want_frames=want_frames, stats=stats)
+    nfail = 0
+    for s, blk, (status, csize, data, frame) in zip(srcs, payloads, res):
+        tt = gpu.table_type(s)
+        if tt == 0:  # > BIO_MAX_VECS segments: LZ4E_compress_default returns 0 -> -EIO
+            assert status == -gpu.EIO and csize == 0
+            nfail += 1
+            continue
+        er, ef, _, _ = oracle_ref.compress(blk, tt)
+        assert status == 0 and csize == er
+        assert data == blk
+        if want_frames:
+            assert frame == ef
+    assert good == len(srcs) - nfail
+    assert stats.reqs_total == len(srcs) and stats.reqs_failed == nfail
+    assert stats.data_in_bytes == sum(len(b) for s, b in zip(srcs, payloads) if gpu.table_type(s))
+    return stats
+
+
+def test_chunk_write_batch_layouts(gpu):
+    rng = np.random.default_rng(404)
+    data = _corpus("mixed", 1 << 20, 41).tobytes()
+    srcs, payloads = [], []
+    sizes = [0, 1, 12, 13, 100, 4096, 4096, 8192, 65536, 65536, 30001, 131072]
+    for i, n in enumerate(sizes):
+        s = int(rng.integers(0, len(data) - n))
+        blk = data[s:s + n]
+        seg = [4096, 512, 1000][i % 3]
+        done = int(rng.integers(0, 64)) if i % 4 == 3 else 0
+        segs = [min(seg, n + done - k) for k in range(0, n + done, seg)] or [16]
+        offs = [int(rng.integers(0, 4096)) for _ in segs]
+        srcs.append(make_sg(blk, segs, offsets=offs, start_done=done, shuffle_seed=i))
+        payloads.append(blk)
+    # 257 segments: rejected like the reference (lz4e_compress.c:274-277)
+    blk = data[:257 * 16]
+    srcs.append(make_sg(blk, [16] * 257))
+    payloads.append(blk)
+    _chunk_check(gpu, srcs, payloads)
+
+
+def test_chunk_write_batch_streamed(gpu):
+    """More input than one 32 MiB pipeline sub-batch: both slots cycle."""
+    bs, nreq = 65536, 800
+    data = corpus.silesia_proxy(nreq * bs, 0x5157)
+    srcs, payloads = [], []
+    for i in range(nreq):
+        blk = data[i * bs:(i + 1) * bs].tobytes()
+        srcs.append(make_sg(blk, [4096] * 16))
+        payloads.append(blk)
+    stats = gpu.ChunkStats()
+    good, res = gpu.chunk_write_batch(srcs, want_frames=True, stats=stats)
+    assert good == nreq and stats.reqs_failed == 0
+    assert all(st == 0 and d == b for (st, _, d, _), b in zip(res, payloads))
+    for i in range(0, nreq, 53):
+        er, ef, _, _ = oracle_ref.compress(payloads[i], BYU16)
+        assert res[i][1] == er and res[i][3] == ef
+    assert stats.frame_bytes == sum(r[1] for r in res)

@@ -40,6 +40,15 @@ LZ4E_DEV uint64_t ballot(bool p) {
     g_wave->bar.arrive_and_wait();
     return m;
 }
+LZ4E_DEV uint64_t match_any6(uint32_t key) {
+    uint64_t m = ~0ull;
+    for (uint32_t b = 0; b < 6; ++b) {
+        const bool bit = (key >> b) & 1;
+        const uint64_t bb = ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return m;
+}
 LZ4E_DEV uint32_t uni(uint32_t v) { return (uint32_t)emu_gather(v, 0); }
 LZ4E_DEV uint32_t lane_val(uint32_t v, uint32_t l) { return (uint32_t)emu_gather(v, l); }
 LZ4E_DEV uint32_t set_lane(uint32_t v, uint32_t x, uint32_t l) {
