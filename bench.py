@@ -240,7 +240,7 @@ def main():
     }
 
     # ---- end to end through the chunk layer (PCIe-inclusive, never `value`) ----
-    if not args.no_e2e:
+    if world == 1 and not args.no_e2e:
         result["end_to_end"] = end_to_end(host, nblk, bs, cls)
 
     # ---- CPU baseline (rank 0, N=1 only) ---------------------------------------

@@ -204,6 +204,25 @@ int lz4e_decompress_batch_dev(const uint8_t *src, const uint64_t *src_off,
 			      int32_t *ret, uint32_t nblocks, void *stream);
 
 /*
+ * LZ4E_decompress_safe into a bio_vec list (the read
+ * side without a bounce buffer).  Decodes compressedSize bytes at `source`
+ * into the segments of `dst` from *dstIter on, with capacity
+ * dstIter->bi_size.  Returns exactly what LZ4E_decompress_safe returns for
+ * that capacity (bytes written, or -(ip - src) - 1 on malformed input,
+ * lz4e/lz4e_decompress.c:449-459); on success *dstIter is advanced by the
+ * return value, on error nothing is written and *dstIter is untouched.
+ */
+int lz4e_decompress_safe_sg(const char *source, struct bio_vec *dst,
+			    struct bvec_iter *dstIter, int compressedSize);
+
+/* Batch form: request i decodes (src[i], csize[i]) into (dst[i],
+ * dstIter[i]); ret[i] as above.  Returns the number of requests with
+ * ret >= 0, or -1 when no GPU is usable. */
+int lz4e_decompress_sg_batch(const char *const *src, const int *csize,
+			     struct bio_vec *const *dst,
+			     struct bvec_iter *const *dstIter, int *ret, int n);
+
+/*
  * Chunk-layer WRITE round trip, batched and streamed.
  * Per request this is the data path of lz4e_write_req_init
  * (lz4e_bdev/lz4e_req.c:144-213): lz4e_chunk_compress_ext

@@ -400,6 +400,39 @@ int LZ4E_decompress_safe(const char* source, char* dest, int compressedSize, int
     return r;
 }
 
+int lz4e_decompress_sg_batch(const char* const* src, const int* csize, struct bio_vec* const* dst,
+                             struct bvec_iter* const* dstIter, int* ret, int n) {
+    if (n <= 0) return 0;
+    // decode into one host staging area, then scatter the successful blocks
+    std::vector<uint64_t> at((size_t)n);
+    uint64_t total = 0;
+    std::vector<int> cap((size_t)n);
+    for (int i = 0; i < n; ++i) {
+        cap[i] = (int)std::min<uint32_t>(dstIter[i]->bi_size, 0x7FFFFFFFu);
+        at[i] = total;
+        total += (uint64_t)cap[i] + 1;
+    }
+    std::vector<char> stage(total + 1);
+    std::vector<char*> dp((size_t)n);
+    for (int i = 0; i < n; ++i) dp[i] = stage.data() + at[i];
+    const int good = lz4e_decompress_batch(src, csize, dp.data(), cap.data(), ret, n);
+    if (good < 0) return -1;
+    for (int i = 0; i < n; ++i) {
+        if (ret[i] < 0) continue;
+        sg_scatter(dst[i], *dstIter[i], reinterpret_cast<const uint8_t*>(dp[i]), (uint32_t)ret[i]);
+        iter_advance(dst[i], dstIter[i], (uint32_t)ret[i]);
+    }
+    return good;
+}
+
+int lz4e_decompress_safe_sg(const char* source, struct bio_vec* dst, struct bvec_iter* dstIter,
+                            int compressedSize) {
+    int r = -1;
+    if (lz4e_decompress_sg_batch(&source, &compressedSize, &dst, &dstIter, &r, 1) < 0)
+        return r < 0 ? r : -1;
+    return r;
+}
+
 int lz4e_compress_batch_dev(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
                             const uint8_t* table_type, uint8_t* dst, const uint64_t* dst_off,
                             const uint32_t* dst_cap, int32_t* ret, uint32_t* aux, uint32_t nblocks,
@@ -458,11 +491,11 @@ constexpr int kEIO = -5, kENOSPC = -28;
 constexpr uint64_t kSubBytes = 32ull << 20;  // input bytes per pipeline sub-batch
 constexpr uint32_t kSubReqs = 16384;         // requests per sub-batch
 
-// Runs f(j) for j in [0, n) on up to 8 host threads when the bytes justify it.
+// Runs f(j) for j in [0, n) on up to 16 host threads when the bytes justify it.
 template <class F>
 void par_for(uint32_t n, uint64_t bytes, F f) {
     const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
-    const uint32_t T = bytes < (4ull << 20) ? 1u : std::min({8u, hw, n});
+    const uint32_t T = bytes < (4ull << 20) ? 1u : std::min({16u, hw, n});
     if (T <= 1) {
         for (uint32_t j = 0; j < n; ++j) f(j);
         return;

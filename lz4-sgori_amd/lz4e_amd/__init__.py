@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "LZ4E_compress_default", "LZ4E_decompress_safe", "lz4e_sg_table_type",
     "lz4e_last_error", "lz4e_gpu_available", "lz4e_compress_sg_batch",
     "lz4e_decompress_batch", "lz4e_compress_batch_dev", "lz4e_decompress_batch_dev",
-    "lz4e_chunk_write_batch",
+    "lz4e_chunk_write_batch", "lz4e_decompress_safe_sg", "lz4e_decompress_sg_batch",
 )
 
 
@@ -135,6 +135,10 @@ def lib() -> ctypes.CDLL:
     L.lz4e_decompress_batch_dev.restype = I32
     L.lz4e_chunk_write_batch.argtypes = [ctypes.POINTER(ChunkRequest), I32, ctypes.POINTER(ChunkStats)]
     L.lz4e_chunk_write_batch.restype = I32
+    L.lz4e_decompress_safe_sg.argtypes = [P, ctypes.POINTER(BioVec), ctypes.POINTER(BvecIter), I32]
+    L.lz4e_decompress_safe_sg.restype = I32
+    L.lz4e_decompress_sg_batch.argtypes = [P, P, P, P, P, I32]
+    L.lz4e_decompress_sg_batch.restype = I32
     _lib = L
     return L
 
@@ -299,6 +303,29 @@ def decompress_batch(frames: Sequence[bytes], caps: Sequence[int]) -> List[Tuple
     if lib().lz4e_decompress_batch(sp, cs, dp, cp, rt, n) < 0:
         raise GpuUnavailable(last_error())
     return [(rt[i], dsts[i].raw[:max(rt[i], 0)]) for i in range(n)]
+
+
+def decompress_safe_sg(source: bytes, dst: SgList, compressed_size: Optional[int] = None) -> int:
+    """lz4e_decompress_safe_sg: decode into dst's segments from dst.it (capacity dst.it.bi_size)."""
+    _require_gpu()
+    csize = len(source) if compressed_size is None else compressed_size
+    src = ctypes.create_string_buffer(bytes(source), max(len(source), 1))
+    return lib().lz4e_decompress_safe_sg(src, dst.bvecs, ctypes.byref(dst.it), csize)
+
+
+def decompress_sg_batch(frames: Sequence[bytes], dsts: Sequence[SgList]) -> List[int]:
+    """lz4e_decompress_sg_batch; returns ret per frame (dst iterators advance on success)."""
+    _require_gpu()
+    n = len(frames)
+    srcs = [ctypes.create_string_buffer(bytes(f), max(len(f), 1)) for f in frames]
+    sp = (ctypes.c_void_p * n)(*[ctypes.addressof(s) for s in srcs])
+    cs = (ctypes.c_int * n)(*[len(f) for f in frames])
+    dp = (ctypes.c_void_p * n)(*[ctypes.addressof(d.bvecs) for d in dsts])
+    ip = (ctypes.c_void_p * n)(*[ctypes.addressof(d.it) for d in dsts])
+    rt = (ctypes.c_int * n)()
+    if lib().lz4e_decompress_sg_batch(sp, cs, dp, ip, rt, n) < 0:
+        raise GpuUnavailable(last_error())
+    return list(rt)
 
 
 def chunk_write_batch(srcs: Sequence[SgList], want_frames: bool = False,

@@ -412,3 +412,65 @@ def test_chunk_write_batch_streamed(gpu):
         er, ef, _, _ = oracle_ref.compress(payloads[i], BYU16)
         assert res[i][1] == er and res[i][3] == ef
     assert stats.frame_bytes == sum(r[1] for r in res)
+
+
+# ---------------------------------------------------------------------------
+# SG-output decompress
+# ---------------------------------------------------------------------------
+
+def test_decompress_sg_layouts_and_codes(gpu):
+    rng = np.random.default_rng(808)
+    data = _corpus("mixed", 1 << 20, 51).tobytes()
+    frames, dsts, blocks, exp = [], [], [], []
+    for i in range(16):
+        n = int(rng.integers(0, 70000))
+        s = int(rng.integers(0, len(data) - n))
+        blk = data[s:s + n]
+        er, ef, _, _ = oracle_ref.compress(blk, BYU16 if n <= 65536 else BYU32)
+        if i % 5 == 4:
+            ef = ef[:len(ef) // 2]  # truncated: the decoder's error code, nothing written
+        cap = n + int(rng.integers(0, 3)) * 100
+        seg = [512, 4096, 1000, 333][i % 4]
+        done = int(rng.integers(0, 100)) if i % 3 == 2 else 0
+        segs = [seg] * (-(-(cap + done) // seg) or 1)
+        offs = [int(rng.integers(0, 4096)) for _ in segs]
+        dsts.append(make_sg(b"", segs, offsets=offs, start_done=done, capacity=cap,
+                            shuffle_seed=i, fill=0xA5))
+        frames.append(ef)
+        blocks.append(blk)
+        exp.append(oracle_ref.decompress(ef, cap))
+    before = [(d.it.as_tuple(), d.read_prefix(sum(d.bvecs[k].bv_len for k in range(d.nseg)))) for d in dsts]
+    rets = gpu.decompress_sg_batch(frames, dsts)
+    for d, blk, (er, eb), r, (it0, raw0) in zip(dsts, blocks, exp, rets, before):
+        assert r == er
+        if r < 0:
+            assert d.it.as_tuple() == it0
+            assert d.read_prefix(len(raw0)) == raw0
+            continue
+        assert r == len(blk)
+        assert gather_from(d, it0, r) == blk
+        assert d.it.bi_size == it0[0] - r
+
+
+def gather_from(d, it0, n):
+    """n bytes of d's segments starting at the ORIGINAL iterator position it0."""
+    size, idx, done = it0
+    out = bytearray()
+    while len(out) < n:
+        b = d.bvecs[idx]
+        take = min(b.bv_len - done, n - len(out))
+        out += ctypes.string_at(b.bv_page + b.bv_offset + done, take)
+        done = 0
+        idx += 1
+    return bytes(out)
+
+
+def test_decompress_safe_sg_single(gpu, test_files):
+    blk = test_files["02.txt"]
+    er, ef, _, _ = oracle_ref.compress(blk, BYU16)
+    d = make_sg(b"", [512] * (-(-len(blk) // 512)), capacity=len(blk), shuffle_seed=3)
+    assert gpu.decompress_safe_sg(ef, d) == len(blk)
+    assert d.read_prefix(len(blk)) == blk
+    assert d.it.bi_size == 0
+    d2 = make_sg(b"", [4096] * 5, capacity=len(blk) - 1)
+    assert gpu.decompress_safe_sg(ef, d2) == oracle_ref.decompress(ef, len(blk) - 1)[0] < 0
