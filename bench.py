@@ -78,7 +78,7 @@ def make_data(gen: str, nbytes: int, seed: int) -> np.ndarray:
 def end_to_end(host: np.ndarray, nblk: int, bs: int, cls: int, reps: int = 3) -> dict:
     """lz4e_chunk_write_batch over the same blocks given as host bio_vec lists
     (16 x 4 KiB segments per 64 KiB block, 128 x 512 B for sg512): SG gather
-    -> H2D -> compress -> decompress -> D2H -> copy-out, two pipeline slots.
+    -> H2D -> compress -> decompress -> D2H -> copy-out, four pipeline slots.
     The host buffers are pageable numpy memory, as a bio's pages would be."""
     import ctypes
     seg = 512 if cls == BYU32 and bs == 65536 else min(bs, 4096)

@@ -230,10 +230,10 @@ int lz4e_decompress_sg_batch(const char *const *src, const int *csize,
  * payload into a LZ4E_COMPRESSBOUND-sized chunk, i.e. never output-limited),
  * then lz4e_chunk_decompress (lz4e_chunk.c:119-137: LZ4_decompress_safe of
  * that frame back into the chunk's contiguous source buffer, whose size must
- * equal the bio's, lz4e_chunk.c:133).  Requests flow through two pipeline
- * slots (pinned staging + HBM buffers + a HIP stream each): the SG gather of
- * one sub-batch overlaps the H2D copy, both kernels and the D2H copy of the
- * other.
+ * equal the bio's, lz4e_chunk.c:133).  Requests flow through four pipeline
+ * slots (pinned staging + HBM buffers + a HIP stream each) in sub-batches of
+ * up to 32 MiB: the SG gather of one sub-batch overlaps the H2D copies,
+ * kernels and D2H copies of the others.
  */
 struct lz4e_chunk_request {
 	const struct bio_vec *src;       /* original bio's bi_io_vec            */

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -490,6 +491,10 @@ namespace {
 constexpr int kEIO = -5, kENOSPC = -28;
 constexpr uint64_t kSubBytes = 32ull << 20;  // input bytes per pipeline sub-batch
 constexpr uint32_t kSubReqs = 16384;         // requests per sub-batch
+// Sub-batches in flight.  A sub-batch's kernels take about the slowest
+// block's parse time whatever their size, so several run side by side on
+// their own streams to keep the GPU full while the host gathers the next.
+constexpr uint32_t kSlots = 4;
 
 // Runs f(j) for j in [0, n) on up to 16 host threads when the bytes justify it.
 template <class F>
@@ -541,7 +546,7 @@ struct ChunkSlot {
 
 struct ChunkCtx {
     std::mutex mu;
-    ChunkSlot slot[2];
+    ChunkSlot slot[kSlots];
     bool ready = false;
     bool init() {
         if (ready) return true;
@@ -560,11 +565,25 @@ ChunkCtx& chunk_ctx() {
 }
 
 // Waits for a slot's sub-batch and hands its results to the requests.
+// LZ4E_CHUNK_PROF=1: per-phase host times of the pipeline on stderr.
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+struct ChunkProf {
+    bool on = getenv("LZ4E_CHUNK_PROF") != nullptr;
+    double wait = 0, out = 0, gather = 0, submit = 0;
+};
+
 bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chunk_stats* st,
-                  int& good) {
+                  int& good, ChunkProf& pr) {
     if (!s.busy) return true;
     s.busy = false;
+    double t0 = pr.on ? now_ms() : 0;
     if (!hip_ok(hipEventSynchronize(s.done), "chunk sync")) return false;
+    double t1 = pr.on ? now_ms() : 0;
+    pr.wait += t1 - t0;
     const uint8_t* hd = static_cast<const uint8_t*>(s.h_data.p);
     const uint8_t* hm = static_cast<const uint8_t*>(s.h_meta.p);
     const int32_t* ret = reinterpret_cast<const int32_t*>(hm + s.meta_ret);
@@ -588,6 +607,7 @@ bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chu
         if (len > 0) std::memcpy(q.data, hd + s.out[j], (size_t)len);
         q.status = 0;
     });
+    if (pr.on) pr.out += now_ms() - t1;
     for (uint32_t j = 0; j < R; ++j) {
         const lz4e_chunk_request& q = reqs[s.req[j]];
         if (q.status == 0) good++;
@@ -624,9 +644,11 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
     int good = 0;
     uint32_t i = 0, k = 0;
     const uint32_t N = (uint32_t)n;
+    ChunkProf pr;
+    const double tstart = pr.on ? now_ms() : 0;
     while (i < N) {
-        ChunkSlot& s = cc.slot[k & 1];
-        if (!chunk_finish(s, reqs, stats, good)) return -1;
+        ChunkSlot& s = cc.slot[k % kSlots];
+        if (!chunk_finish(s, reqs, stats, good, pr)) return -1;
         // ---- form the sub-batch: requests [i, e) ----
         s.req.clear();
         s.fr.clear();
@@ -677,10 +699,13 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
         uint8_t* hd = static_cast<uint8_t*>(s.h_data.p);
         uint8_t* hm = static_cast<uint8_t*>(s.h_meta.p);
         // ---- gather (overlaps the other slot's GPU work) ----
+        const double tg = pr.on ? now_ms() : 0;
         par_for(R, ib, [&](uint32_t j) {
             const lz4e_chunk_request& q = reqs[s.req[j]];
             sg_gather(q.src, *q.srcIter, hd + in[j], q.srcIter->bi_size);
         });
+        const double ts = pr.on ? now_ms() : 0;
+        pr.gather += ts - tg;
         for (uint32_t j = 0; j < R; ++j) {
             const uint32_t len = reqs[s.req[j]].srcIter->bi_size;
             reinterpret_cast<uint64_t*>(hm + m.in_off)[j] = in[j];
@@ -730,9 +755,14 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
             return -1;
         s.busy = true;
         k++;
+        if (pr.on) pr.submit += now_ms() - ts;
     }
-    for (uint32_t t = 0; t < 2; ++t)
-        if (!chunk_finish(cc.slot[(k + t) & 1], reqs, stats, good)) return -1;
+    for (uint32_t t = 0; t < kSlots; ++t)
+        if (!chunk_finish(cc.slot[(k + t) % kSlots], reqs, stats, good, pr)) return -1;
+    if (pr.on)
+        fprintf(stderr, "lz4e chunk: %u sub-batches, total %.2f ms: gpu wait %.2f, copy-out %.2f, "
+                "gather %.2f, submit %.2f\n", k, now_ms() - tstart, pr.wait, pr.out, pr.gather,
+                pr.submit);
     return good;
 }
 
