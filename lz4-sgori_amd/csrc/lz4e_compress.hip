@@ -277,6 +277,39 @@ LZ4E_DEV uint32_t fwd_match(const uint32_t* a, const uint32_t* b, uint32_t lim) 
     return m == kFwd ? (kFwd | kLong) : m;
 }
 
+// fwd_match of my kFwd bytes against those of window lane cl (every lane
+// calls it; `active` lanes use the result).  Lane cl's dwords 4..7 are only
+// fetched (ds_bpermute) when some active lane's first 16 bytes all match:
+// most matches end earlier.
+LZ4E_DEV uint32_t fwd_match_lane(const uint32_t* dv, uint32_t cl, uint32_t lim, bool active) {
+    uint32_t g[4];
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i) g[i] = shfl(dv[i], cl);
+    uint32_t m = 16;
+#pragma unroll
+    for (int i = 3; i >= 1; --i) {
+        const uint32_t x = dv[i] ^ g[i];
+        if (x) m = 4 * (uint32_t)i + ((uint32_t)__builtin_ctz(x) >> 3);
+    }
+    const bool eq0 = dv[0] == g[0];
+    if (ballot(active && eq0 && m == 16)) {
+        uint32_t h[kFwdW - 4];
+#pragma unroll
+        for (uint32_t i = 0; i < kFwdW - 4; ++i) h[i] = shfl(dv[4 + i], cl);
+        if (m == 16) {
+            m = kFwd;
+#pragma unroll
+            for (int i = (int)kFwdW - 1; i >= 4; --i) {
+                const uint32_t x = dv[i] ^ h[i - 4];
+                if (x) m = 4 * (uint32_t)i + ((uint32_t)__builtin_ctz(x) >> 3);
+            }
+        }
+    }
+    if (!eq0) return 0;
+    if (m >= lim) return lim;
+    return m == kFwd ? (kFwd | kLong) : m;
+}
+
 // Equal bytes at the top of two dwords (backward catch-up, up to 4).
 LZ4E_DEV uint32_t back4(uint32_t a, uint32_t b) {
     const uint32_t x = a ^ b;
@@ -510,14 +543,12 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                                 const uint64_t pm =
                                     ((clash >> lane) & 1) ? (same & Pg & lanes_below) : 0;
                                 const uint32_t cl = pm ? 63 - (uint32_t)__builtin_clzll(pm) : lane;
-                                uint32_t gv[kFwdW];
-#pragma unroll
-                                for (uint32_t i = 0; i < kFwdW; ++i) gv[i] = shfl(dv[i], cl);
                                 const uint32_t gm1 = shfl(dm1, cl);
+                                const uint32_t fm = fwd_match_lane(dv, cl, lim, pm && valid);
                                 uint32_t vc = c0, vm = ml, vb = bk;
                                 if (pm) {
                                     vc = B + cl;
-                                    vm = valid ? fwd_match(dv, gv, lim) : 0;
+                                    vm = valid ? fm : 0;
                                     vb = (p >= 4 && B + cl >= 4) ? back4(dm1, gm1) : kNoBk;
                                 }
                                 chain_tables(vc, vm, vb, fc, fe, jv);
@@ -671,13 +702,11 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                     const uint64_t prior_l = put | (lane > k0 ? lane_range(k0, lane - 1) : 0);
                     const uint64_t pm = isc ? (same & prior_l & lanes_below) : 0;
                     const uint32_t cl = pm ? 63 - (uint32_t)__builtin_clzll(pm) : lane;
-                    uint32_t gv[kFwdW];
-#pragma unroll
-                    for (uint32_t i = 0; i < kFwdW; ++i) gv[i] = shfl(dv[i], cl);
                     const uint32_t gm1 = shfl(dm1, cl);
+                    const uint32_t fm = fwd_match_lane(dv, cl, lim, pm != 0);
                     if (pm) {
                         vc = B + cl;
-                        vm = fwd_match(dv, gv, lim);
+                        vm = fm;
                         vb = (p >= 4 && B + cl >= 4) ? back4(dm1, gm1) : kNoBk;
                     }
                 }
