@@ -232,7 +232,7 @@ int lz4e_decompress_sg_batch(const char *const *src, const int *csize,
  * that frame back into the chunk's contiguous source buffer, whose size must
  * equal the bio's, lz4e_chunk.c:133).  Requests flow through four pipeline
  * slots (pinned staging + HBM buffers + a HIP stream each) in sub-batches of
- * up to 32 MiB: the SG gather of one sub-batch overlaps the H2D copies,
+ * up to 64 MiB: the SG gather of one sub-batch overlaps the H2D copies,
  * kernels and D2H copies of the others.
  */
 struct lz4e_chunk_request {

@@ -489,7 +489,7 @@ int lz4e_decompress_batch_dev(const uint8_t* src, const uint64_t* src_off, const
 namespace {
 
 constexpr int kEIO = -5, kENOSPC = -28;
-constexpr uint64_t kSubBytes = 32ull << 20;  // input bytes per pipeline sub-batch
+constexpr uint64_t kSubBytes = 64ull << 20;  // input bytes per pipeline sub-batch
 constexpr uint32_t kSubReqs = 16384;         // requests per sub-batch
 // Sub-batches in flight.  A sub-batch's kernels take about the slowest
 // block's parse time whatever their size, so several run side by side on

@@ -396,8 +396,8 @@ def test_chunk_write_batch_layouts(gpu):
 
 
 def test_chunk_write_batch_streamed(gpu):
-    """More input than one 32 MiB pipeline sub-batch: both slots cycle."""
-    bs, nreq = 65536, 800
+    """More input than one 64 MiB pipeline sub-batch: the slots cycle."""
+    bs, nreq = 65536, 2200
     data = corpus.silesia_proxy(nreq * bs, 0x5157)
     srcs, payloads = [], []
     for i in range(nreq):
@@ -408,7 +408,7 @@ def test_chunk_write_batch_streamed(gpu):
     good, res = gpu.chunk_write_batch(srcs, want_frames=True, stats=stats)
     assert good == nreq and stats.reqs_failed == 0
     assert all(st == 0 and d == b for (st, _, d, _), b in zip(res, payloads))
-    for i in range(0, nreq, 53):
+    for i in range(0, nreq, 157):
         er, ef, _, _ = oracle_ref.compress(payloads[i], BYU16)
         assert res[i][1] == er and res[i][3] == ef
     assert stats.frame_bytes == sum(r[1] for r in res)
