@@ -489,6 +489,31 @@ int lz4e_decompress_batch_dev(const uint8_t* src, const uint64_t* src_off, const
 namespace {
 
 constexpr int kEIO = -5, kENOSPC = -28;
+
+// Device -> pinned host copy as a kernel on the slot's own stream.  The DMA
+// engine serves every stream's copies in submission order, so a D2H that
+// waits for its sub-batch's kernels would hold up the next sub-batch's H2D
+// (measured: the whole pipeline ran serialised).  Only H2D copies go to the
+// DMA engine; results come back through the host mapping of the pinned
+// buffer, 16 bytes per lane.
+__global__ __launch_bounds__(256) void copy_out_kernel(const uint4* __restrict__ src,
+                                                       uint4* __restrict__ dst, uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+        dst[i] = src[i];
+}
+
+// Copies bytes [off, off + n) of the slot's data buffer (16-B aligned offsets
+// and sizes) from HBM to the same offsets of its pinned twin.
+hipError_t copy_out(void* host_dev, const void* dev, uint64_t off, uint64_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t n16 = (n + 15) / 16;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(1024, (n16 + 255) / 256);
+    hipLaunchKernelGGL(copy_out_kernel, dim3(blocks), dim3(256), 0, st,
+                       reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(dev) + off),
+                       reinterpret_cast<uint4*>(static_cast<uint8_t*>(host_dev) + off), n16);
+    return hipGetLastError();
+}
 constexpr uint64_t kSubBytes = 64ull << 20;  // input bytes per pipeline sub-batch
 constexpr uint32_t kSubReqs = 16384;         // requests per sub-batch
 // Sub-batches in flight.  A sub-batch's kernels take about the slowest
@@ -536,6 +561,7 @@ struct ChunkSlot {
     hipEvent_t done = nullptr;
     HostBuf h_data, h_meta;
     DevBuf d_data, d_meta;
+    void* h_dev = nullptr;  // h_data as the device sees it
     bool busy = false;
     bool want_frames = false;
     std::vector<uint32_t> req;        // request index per entry
@@ -694,7 +720,8 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
         const ChunkMeta m(R);
         const uint64_t total = ib + fb + ob;
         if (!s.h_data.ensure(total) || !s.d_data.ensure(total) || !s.h_meta.ensure(m.total) ||
-            !s.d_meta.ensure(m.total))
+            !s.d_meta.ensure(m.total) ||
+            !hip_ok(hipHostGetDevicePointer(&s.h_dev, s.h_data.p, 0), "hipHostGetDevicePointer"))
             return -1;
         uint8_t* hd = static_cast<uint8_t*>(s.h_data.p);
         uint8_t* hm = static_cast<uint8_t*>(s.h_meta.p);
@@ -747,10 +774,8 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
             !hip_ok(lz4e::launch_decompress(da, s.stream), "decompress launch") ||
             !hip_ok(hipMemcpyAsync(hm + m.ret, dm + m.ret, m.total - m.ret, hipMemcpyDeviceToHost,
                                    s.stream), "D2H meta") ||
-            (frames && !hip_ok(hipMemcpyAsync(hd + ib, dd + ib, fb, hipMemcpyDeviceToHost, s.stream),
-                               "D2H frames")) ||
-            !hip_ok(hipMemcpyAsync(hd + ib + fb, dd + ib + fb, ob, hipMemcpyDeviceToHost, s.stream),
-                    "D2H data") ||
+            (frames && !hip_ok(copy_out(s.h_dev, dd, ib, fb, s.stream), "D2H frames")) ||
+            !hip_ok(copy_out(s.h_dev, dd, ib + fb, ob, s.stream), "D2H data") ||
             !hip_ok(hipEventRecord(s.done, s.stream), "event record"))
             return -1;
         s.busy = true;
