@@ -576,10 +576,19 @@ struct ChunkCtx {
     bool ready = false;
     bool init() {
         if (ready) return true;
-        for (auto& s : slot)
-            if (!hip_ok(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking), "hipStreamCreate") ||
+        // Half of the slots on the high-priority stream pool: streams of one
+        // priority share few hardware queues (two slots per queue were seen
+        // serialising their kernels), the other pool brings its own.
+        int lo = 0, hi = 0;
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+        for (uint32_t i = 0; i < kSlots; ++i) {
+            ChunkSlot& s = slot[i];
+            if (!hip_ok(hipStreamCreateWithPriority(&s.stream, hipStreamNonBlocking,
+                                                    (i & 1) ? hi : lo),
+                        "hipStreamCreate") ||
                 !hip_ok(hipEventCreateWithFlags(&s.done, hipEventDisableTiming), "hipEventCreate"))
                 return false;
+        }
         ready = true;
         return true;
     }
