@@ -51,6 +51,15 @@ LZ4E_DEV uint64_t match_any6(uint32_t key) {
     }
     return m;
 }
+// Wave issue priority from the share of its work still ahead (q: quarters
+// done, 0..3): the wave furthest behind wins issue slots on its SIMD, which
+// shortens the batch's longest block ("least progress first").
+LZ4E_DEV void wave_prio_for(uint32_t q) {
+    if (q == 0) __builtin_amdgcn_s_setprio(3);
+    else if (q == 1) __builtin_amdgcn_s_setprio(2);
+    else if (q == 2) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+}
 // ds_permute: lane l sends v to lane dst (l's own choice); a lane nobody
 // sends to receives an unspecified value.
 LZ4E_DEV uint32_t push_lane(uint32_t v, uint32_t dst) {

@@ -40,6 +40,7 @@ LZ4E_DEV uint64_t ballot(bool p) {
     g_wave->bar.arrive_and_wait();
     return m;
 }
+LZ4E_DEV void wave_prio_for(uint32_t) {}
 LZ4E_DEV uint64_t match_any6(uint32_t key) {
     uint64_t m = ~0ull;
     for (uint32_t b = 0; b < 6; ++b) {
