@@ -12,7 +12,8 @@
  * Both single-call entry points run on the GPU (gfx950): the host shim
  * gathers the bio_vec segments into pinned staging, copies them to HBM,
  * launches the hand-written HIP kernel and scatters the frame back into the
- * destination bio_vecs.  There is no CPU codec behind these symbols; when no
+ * destination bio_vecs.  Like the reference they are reentrant: concurrent
+ * callers each lease their own HIP stream and staging (no global lock).  There is no CPU codec behind these symbols; when no
  * GPU is usable they fail (compress returns 0, decompress returns a negative
  * value) and lz4e_last_error() says why.
  *
@@ -247,18 +248,26 @@ struct lz4e_chunk_request {
 			      -ENOSPC (-28) when frame_cap < comp_size          */
 };
 
-/* Counters of one call, in the spirit of lz4e_bdev/lz4e_stats.c:39-52
- * (reqs_total / reqs_failed / data_in_bytes of the requests handled here;
- * frame_bytes = sum of comp_size). */
+/* Write-side counters, the reference's struct lz4e_stats
+ * (lz4e_bdev/include/lz4e_stats.h:17-22) updated as lz4e_stats_update does
+ * at bio completion (lz4e_bdev/lz4e_stats.c:39-52): every request counts in
+ * reqs_total, a failed one in reqs_failed only; a successful one adds the
+ * bi_vcnt of the bio the reference completes (its src buffer re-added by
+ * lz4e_add_buf_to_bio, lz4e_req.c:191-197: one merged bio_vec per
+ * contiguous non-empty buffer) to vec_count and its size to data_in_bytes.
+ * frame_bytes (not in the reference) = sum of comp_size. */
 struct lz4e_chunk_stats {
 	uint64_t reqs_total;
 	uint64_t reqs_failed;
+	uint64_t vec_count;
 	uint64_t data_in_bytes;
 	uint64_t frame_bytes;
 };
 
-/* Returns the number of requests with status 0, or -1 when no GPU is usable
- * (every status is then -EIO).  `stats` is nullable; it is added to. */
+/* Returns the number of requests with status 0, or -1 on failure (no usable
+ * GPU, or a HIP error part way through): every status is then -EIO, every
+ * comp_size 0, `stats` is left untouched and nothing of the call is still
+ * in flight.  `stats` is nullable; on success it is added to. */
 int lz4e_chunk_write_batch(struct lz4e_chunk_request *reqs, int n,
 			   struct lz4e_chunk_stats *stats);
 

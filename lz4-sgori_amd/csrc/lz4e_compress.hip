@@ -1008,7 +1008,7 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
                                                       const uint32_t* __restrict__ dst_cap,
                                                       int32_t* __restrict__ ret,
                                                       uint32_t* __restrict__ aux, uint32_t nblocks,
-                                                      uint64_t* __restrict__ dbg) {
+                                                      uint32_t max_len, uint64_t* __restrict__ dbg) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t b = blockIdx.x;
     if (b >= nblocks) return;
@@ -1022,9 +1022,12 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
     uint64_t* dbg_slot = dbg ? dbg + 8 * (size_t)b : nullptr;
 
     const bool tt_ok = (tt == kByU16 && n <= 65536) || tt == kByU32 || tt == kByU64;
-    if (n > kMaxInput || (n >= kMinLength && !tt_ok)) {
+    // the launch sized LDS (staging mode) for blocks of at most max_len bytes
+    const bool fits = !kLdsInput || n <= max_len;
+    if (n > kMaxInput || (n >= kMinLength && !tt_ok) || !fits) {
         // Input too large (lz4e_compress.c:245-248) returns 0; a malformed
-        // descriptor (class/length the SG rules cannot produce) returns -1.
+        // descriptor (class/length the SG rules cannot produce, or a block
+        // longer than the batch's max_len) returns -1.
         if (lane == 0) ret[b] = n > kMaxInput ? 0 : -1;
         return;
     }
@@ -1064,11 +1067,11 @@ hipError_t launch_compress_impl(const CompressBatch& a, hipStream_t stream, uint
     if (lds_input) {
         hipLaunchKernelGGL((compress_kernel<true, kStamps>), grid, block, lds, stream, a.src,
                            a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.aux, a.nblocks, dbg);
+                           a.aux, a.nblocks, a.max_len, dbg);
     } else {
         hipLaunchKernelGGL((compress_kernel<false, kStamps>), grid, block, lds, stream, a.src,
                            a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.aux, a.nblocks, dbg);
+                           a.aux, a.nblocks, a.max_len, dbg);
     }
     return hipGetLastError();
 }

@@ -2,19 +2,24 @@
 //
 // Single-call entry points keep the reference's synchronous, per-request
 // contract (lz4e_bdev/lz4e_chunk.c:139-159 calls LZ4E_compress_default once
-// per WRITE bio): gather the SG segments into pinned staging, one H2D copy,
-// one kernel launch, one D2H copy, scatter into the destination segments.
-// The batched entry points amortise that over many requests; the *_dev
-// forms launch straight on device-resident buffers.
+// per WRITE bio) and its reentrancy: each call leases its own stream and
+// staging from a pool (no process-wide lock), gathers the SG segments into
+// pinned staging, makes one H2D copy, launches the kernel, and brings back
+// the results -- exactly the bytes produced -- through the host mapping of
+// the pinned buffer, then scatters into the destination segments.  The
+// batched entry points amortise that over many requests; the *_dev forms
+// launch straight on device-resident buffers.
 //
 // There is no CPU codec here: without a usable gfx950 device every entry
 // point fails (compress 0, decompress < 0) and lz4e_last_error() says why.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -70,52 +75,138 @@ struct HostBuf {
     }
 };
 
-// One process-wide context: the device, a stream and staging buffers.
-struct Ctx {
-    std::mutex mu;
-    int state = 0;  // 0 unknown, 1 ok, -1 unusable
+// Device check, once per process: the library only runs on gfx950.
+struct DeviceGate {
+    std::once_flag once;
+    bool ok = false;
     std::string why;
-    hipStream_t stream = nullptr;
-    DevBuf d_data, d_meta;
-    HostBuf h_data, h_meta;
+    bool check() {
+        std::call_once(once, [this] {
+            int n = 0;
+            if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+                why = "lz4e: no HIP device visible";
+                return;
+            }
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            hipDeviceProp_t prop;
+            if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+                std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+                why = std::string("lz4e: device is not gfx950 (") + prop.gcnArchName + ")";
+                return;
+            }
+            ok = true;
+        });
+        if (!ok) set_err(why);
+        return ok;
+    }
+};
 
-    bool init() {
-        if (state == 1) return true;
-        if (state == -1) {
-            set_err(why);
-            return false;
-        }
-        int n = 0;
-        if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
-            why = "lz4e: no HIP device visible";
-            state = -1;
-            set_err(why);
-            return false;
-        }
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
-            std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-            why = std::string("lz4e: device is not gfx950 (") + prop.gcnArchName + ")";
-            state = -1;
-            set_err(why);
-            return false;
-        }
-        if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
-            why = "lz4e: hipStreamCreate failed";
-            state = -1;
-            set_err(why);
-            return false;
-        }
-        state = 1;
+DeviceGate& gate() {
+    static DeviceGate g;
+    return g;
+}
+
+// Per-call resources of the host entry points: a stream and growable pinned
+// + HBM staging.  Calls lease one from a per-device pool for their duration,
+// so concurrent callers (the reference is reentrant given distinct wrkmem,
+// called from every submitting CPU: lz4e_bdev/lz4e_dev.c:174 ->
+// lz4e_req.c:177) run side by side on their own streams; the pool only
+// grows to the peak concurrency.  Contexts live until process exit.
+struct CallCtx {
+    int dev = 0;
+    hipStream_t stream = nullptr;
+    DevBuf d;      // [inputs | descriptors in | results | outputs]
+    HostBuf h;     // pinned twin of d
+    void* h_dev = nullptr;  // h as the device sees it (results come back by kernel)
+    bool grow(size_t bytes) {
+        if (!d.ensure(bytes)) return false;
+        const void* old = h.p;
+        if (!h.ensure(bytes)) return false;
+        if (h.p != old || !h_dev)
+            return hip_ok(hipHostGetDevicePointer(&h_dev, h.p, 0), "hipHostGetDevicePointer");
         return true;
     }
 };
 
-Ctx& ctx() {
-    static Ctx c;
-    return c;
+struct CtxPool {
+    std::mutex mu;
+    std::vector<CallCtx*> free_;
+};
+
+CtxPool& pool() {
+    static CtxPool p;
+    return p;
+}
+
+// RAII lease of a CallCtx on the calling thread's current device.
+struct Lease {
+    CallCtx* c = nullptr;
+    bool acquire() {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        {
+            std::lock_guard<std::mutex> lk(pool().mu);
+            auto& fl = pool().free_;
+            for (size_t i = 0; i < fl.size(); ++i)
+                if (fl[i]->dev == dev) {
+                    c = fl[i];
+                    fl.erase(fl.begin() + (long)i);
+                    return true;
+                }
+        }
+        CallCtx* n = new CallCtx;
+        n->dev = dev;
+        if (!hip_ok(hipStreamCreateWithFlags(&n->stream, hipStreamNonBlocking), "hipStreamCreate")) {
+            delete n;
+            return false;
+        }
+        c = n;
+        return true;
+    }
+    ~Lease() {
+        if (!c) return;
+        std::lock_guard<std::mutex> lk(pool().mu);
+        pool().free_.push_back(c);
+    }
+};
+
+// Copies blocks back into the host mapping of a pinned buffer: block b moves
+// len[b] bytes (nothing when len[b] <= 0) from dev + off[b] to
+// host + off[b], rounded up to 16 B (offsets are 16-B aligned and every slot
+// has >= 16 B of slack).  Only the bytes that exist come back over PCIe --
+// not the whole capacity -- and no DMA copy waits behind another stream's.
+__global__ __launch_bounds__(256) void copy_blocks_kernel(const uint8_t* __restrict__ dev,
+                                                          uint8_t* __restrict__ host,
+                                                          const uint64_t* __restrict__ off,
+                                                          const int32_t* __restrict__ len,
+                                                          uint32_t n) {
+    const uint32_t b = blockIdx.x;
+    if (b >= n) return;
+    const int32_t l = len[b];
+    if (l <= 0) return;
+    const uint4* s = reinterpret_cast<const uint4*>(dev + off[b]);
+    uint4* d = reinterpret_cast<uint4*>(host + off[b]);
+    const uint32_t n16 = ((uint32_t)l + 15) / 16;
+    for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) d[i] = s[i];
+}
+
+// Raw copy of n bytes (16-B aligned offsets, n rounded up to 16 B).
+__global__ __launch_bounds__(256) void copy_flat_kernel(const uint4* __restrict__ src,
+                                                        uint4* __restrict__ dst, uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
+        dst[i] = src[i];
+}
+
+hipError_t copy_flat(void* host_dev, const void* dev, uint64_t off, uint64_t n, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    const uint64_t n16 = (n + 15) / 16;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(1024, (n16 + 255) / 256);
+    hipLaunchKernelGGL(copy_flat_kernel, dim3(blocks), dim3(256), 0, st,
+                       reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(dev) + off),
+                       reinterpret_cast<uint4*>(static_cast<uint8_t*>(host_dev) + off), n16);
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -185,18 +276,19 @@ int table_type_of(const struct bio_vec* bv, const struct bvec_iter* it) {
     return tt;
 }
 
-// Metadata block layout for a batch of R blocks (device + pinned host):
+// Descriptor block of a batch of R blocks, at `base` inside a staging
+// buffer: the inputs the kernels read, then the results they write.
 struct MetaLayout {
     size_t src_off, src_len, ttype, dst_off, dst_cap, ret, aux, total;
-    explicit MetaLayout(uint32_t R) {
-        size_t o = 0;
-        src_off = o; o += align16(8ull * R);
-        src_len = o; o += align16(4ull * R);
-        ttype = o;   o += align16(1ull * R);
-        dst_off = o; o += align16(8ull * R);
-        dst_cap = o; o += align16(4ull * R);
-        ret = o;     o += align16(4ull * R);
-        aux = o;     o += align16(8ull * R);
+    MetaLayout(uint32_t R, size_t base) {
+        size_t o = base;
+        src_off = o;  o += align16(8ull * R);
+        src_len = o;  o += align16(4ull * R);
+        ttype = o;    o += align16(1ull * R);
+        dst_off = o;  o += align16(8ull * R);
+        dst_cap = o;  o += align16(4ull * R);
+        ret = o;      o += align16(4ull * R);
+        aux = o;      o += align16(8ull * R);
         total = o;
     }
 };
@@ -207,11 +299,7 @@ extern "C" {
 
 const char* lz4e_last_error(void) { return g_err.c_str(); }
 
-int lz4e_gpu_available(void) {
-    Ctx& c = ctx();
-    std::lock_guard<std::mutex> lk(c.mu);
-    return c.init() ? 1 : 0;
-}
+int lz4e_gpu_available(void) { return gate().check() ? 1 : 0; }
 
 int lz4e_sg_table_type(const struct bio_vec* src, const struct bvec_iter* it) {
     return table_type_of(src, it);
@@ -219,91 +307,87 @@ int lz4e_sg_table_type(const struct bio_vec* src, const struct bvec_iter* it) {
 
 int lz4e_compress_sg_batch(struct lz4e_sg_request* reqs, int n) {
     if (n <= 0) return 0;
-    Ctx& c = ctx();
-    std::lock_guard<std::mutex> lk(c.mu);
     g_err.clear();
-    if (!c.init()) return -1;
+    if (!gate().check()) return -1;
+    for (int i = 0; i < n; ++i) reqs[i].ret = 0;
 
-    const uint32_t R = (uint32_t)n;
-    std::vector<uint64_t> src_off(R), dst_off(R);
-    std::vector<uint32_t> src_len(R), dst_cap(R), dst_slot(R);
-    std::vector<uint8_t> ttype(R), live(R);
-    uint64_t so = 0, dso = 0;
-    uint32_t max_len = 0;
-    for (uint32_t i = 0; i < R; ++i) {
-        lz4e_sg_request& q = reqs[i];
-        q.ret = 0;
-        const uint32_t len = q.srcIter->bi_size;
-        int tt = LZ4E_TABLE_BYU16;
-        live[i] = 0;
-        if (len > LZ4E_MAX_INPUT_SIZE) continue;                                   // :245-248
-        if (len >= 13 && (tt = table_type_of(q.src, q.srcIter)) == 0) continue;    // :274-277
-        live[i] = 1;
-        src_len[i] = len;
-        ttype[i] = (uint8_t)tt;
-        dst_cap[i] = q.dstIter->bi_size;
-        dst_slot[i] = std::min(dst_cap[i], bound_of(len)) + 64;
-        src_off[i] = so;
-        so += align16(len);
-        dst_off[i] = dso;
-        dso += align16(dst_slot[i]);
-        max_len = std::max(max_len, len);
-    }
-    // Compact to the live requests.
+    // Live requests (the others return 0 before touching the GPU).
     std::vector<uint32_t> map;
-    for (uint32_t i = 0; i < R; ++i)
-        if (live[i]) map.push_back(i);
+    std::vector<uint8_t> ttype;
+    for (uint32_t i = 0; i < (uint32_t)n; ++i) {
+        const uint32_t len = reqs[i].srcIter->bi_size;
+        int tt = LZ4E_TABLE_BYU16;
+        if (len > LZ4E_MAX_INPUT_SIZE) continue;                                        // :245-248
+        if (len >= 13 && (tt = table_type_of(reqs[i].src, reqs[i].srcIter)) == 0) continue;  // :274-277
+        map.push_back(i);
+        ttype.push_back((uint8_t)tt);
+    }
     const uint32_t L = (uint32_t)map.size();
     if (L == 0) return 0;
-    MetaLayout ml2(L);
-    const size_t data_bytes = so + dso;
-    if (!c.h_data.ensure(data_bytes) || !c.d_data.ensure(data_bytes) ||
-        !c.h_meta.ensure(ml2.total) || !c.d_meta.ensure(ml2.total))
-        return -1;
-    uint8_t* hd = static_cast<uint8_t*>(c.h_data.p);
-    uint8_t* hm = static_cast<uint8_t*>(c.h_meta.p);
+
+    // One staging image, host and device alike:
+    //   [inputs | descriptors | ret/aux | frames]
+    // one H2D copy of everything before ret, the compress kernel, and two
+    // copy-back kernels: ret/aux, then exactly ret[i] bytes of each frame.
+    std::vector<uint64_t> so(L), fo(L);
+    uint64_t s = 0, f = 0;
+    uint32_t max_len = 0;
     for (uint32_t j = 0; j < L; ++j) {
-        const uint32_t i = map[j];
-        sg_gather(reqs[i].src, *reqs[i].srcIter, hd + src_off[i], src_len[i]);
-        reinterpret_cast<uint64_t*>(hm + ml2.src_off)[j] = src_off[i];
-        reinterpret_cast<uint32_t*>(hm + ml2.src_len)[j] = src_len[i];
-        (hm + ml2.ttype)[j] = ttype[i];
-        reinterpret_cast<uint64_t*>(hm + ml2.dst_off)[j] = so + dst_off[i];
-        reinterpret_cast<uint32_t*>(hm + ml2.dst_cap)[j] = dst_cap[i];
+        const lz4e_sg_request& q = reqs[map[j]];
+        const uint32_t len = q.srcIter->bi_size;
+        so[j] = s;
+        s += align16(len);
+        fo[j] = f;
+        f += align16((uint64_t)std::min(q.dstIter->bi_size, bound_of(len)) + 64);
+        max_len = std::max(max_len, len);
     }
-    uint8_t* dd = static_cast<uint8_t*>(c.d_data.p);
-    uint8_t* dm = static_cast<uint8_t*>(c.d_meta.p);
-    if (!hip_ok(hipMemcpyAsync(dd, hd, so, hipMemcpyHostToDevice, c.stream), "H2D data") ||
-        !hip_ok(hipMemcpyAsync(dm, hm, ml2.ret, hipMemcpyHostToDevice, c.stream), "H2D meta"))
+    const MetaLayout m(L, s);
+    const size_t fbase = m.total;
+    Lease ls;
+    if (!ls.acquire()) return -1;
+    CallCtx& c = *ls.c;
+    if (!c.grow(fbase + f)) return -1;
+    uint8_t* hd = static_cast<uint8_t*>(c.h.p);
+    for (uint32_t j = 0; j < L; ++j) {
+        const lz4e_sg_request& q = reqs[map[j]];
+        const uint32_t len = q.srcIter->bi_size;
+        sg_gather(q.src, *q.srcIter, hd + so[j], len);
+        reinterpret_cast<uint64_t*>(hd + m.src_off)[j] = so[j];
+        reinterpret_cast<uint32_t*>(hd + m.src_len)[j] = len;
+        (hd + m.ttype)[j] = ttype[j];
+        reinterpret_cast<uint64_t*>(hd + m.dst_off)[j] = fbase + fo[j];
+        reinterpret_cast<uint32_t*>(hd + m.dst_cap)[j] = q.dstIter->bi_size;
+    }
+    uint8_t* dd = static_cast<uint8_t*>(c.d.p);
+    const lz4e::CompressBatch a{dd,
+                                reinterpret_cast<const uint64_t*>(dd + m.src_off),
+                                reinterpret_cast<const uint32_t*>(dd + m.src_len),
+                                dd + m.ttype,
+                                dd,
+                                reinterpret_cast<const uint64_t*>(dd + m.dst_off),
+                                reinterpret_cast<const uint32_t*>(dd + m.dst_cap),
+                                reinterpret_cast<int32_t*>(dd + m.ret),
+                                reinterpret_cast<uint32_t*>(dd + m.aux),
+                                L,
+                                max_len};
+    if (!hip_ok(hipMemcpyAsync(dd, hd, m.ret, hipMemcpyHostToDevice, c.stream), "H2D") ||
+        !hip_ok(lz4e::launch_compress(a, c.stream), "compress launch") ||
+        !hip_ok(copy_flat(c.h_dev, dd, m.ret, m.total - m.ret, c.stream), "copy-back meta"))
         return -1;
-    lz4e::CompressBatch a{dd,
-                          reinterpret_cast<const uint64_t*>(dm + ml2.src_off),
-                          reinterpret_cast<const uint32_t*>(dm + ml2.src_len),
-                          dm + ml2.ttype,
-                          dd,
-                          reinterpret_cast<const uint64_t*>(dm + ml2.dst_off),
-                          reinterpret_cast<const uint32_t*>(dm + ml2.dst_cap),
-                          reinterpret_cast<int32_t*>(dm + ml2.ret),
-                          reinterpret_cast<uint32_t*>(dm + ml2.aux),
-                          L,
-                          max_len};
-    if (!hip_ok(lz4e::launch_compress(a, c.stream), "compress launch")) return -1;
-    if (!hip_ok(hipMemcpyAsync(hm + ml2.ret, dm + ml2.ret, ml2.total - ml2.ret,
-                               hipMemcpyDeviceToHost, c.stream), "D2H meta") ||
-        !hip_ok(hipMemcpyAsync(hd + so, dd + so, dso, hipMemcpyDeviceToHost, c.stream), "D2H data") ||
+    hipLaunchKernelGGL(copy_blocks_kernel, dim3(L), dim3(256), 0, c.stream, dd,
+                       static_cast<uint8_t*>(c.h_dev),
+                       reinterpret_cast<const uint64_t*>(dd + m.dst_off),
+                       reinterpret_cast<const int32_t*>(dd + m.ret), L);
+    if (!hip_ok(hipGetLastError(), "copy-back frames") ||
         !hip_ok(hipStreamSynchronize(c.stream), "compress sync"))
         return -1;
     int ok = 0;
     for (uint32_t j = 0; j < L; ++j) {
-        const uint32_t i = map[j];
-        lz4e_sg_request& q = reqs[i];
-        const int32_t r = reinterpret_cast<const int32_t*>(hm + ml2.ret)[j];
-        const uint32_t* aux = reinterpret_cast<const uint32_t*>(hm + ml2.aux) + 2 * j;
-        if (r <= 0) {
-            q.ret = 0;
-            continue;
-        }
-        sg_scatter(q.dst, *q.dstIter, hd + so + dst_off[i], (uint32_t)r);
+        lz4e_sg_request& q = reqs[map[j]];
+        const int32_t r = reinterpret_cast<const int32_t*>(hd + m.ret)[j];
+        const uint32_t* aux = reinterpret_cast<const uint32_t*>(hd + m.aux) + 2 * j;
+        if (r <= 0) continue;
+        sg_scatter(q.dst, *q.dstIter, hd + fbase + fo[j], (uint32_t)r);
         iter_advance(q.src, q.srcIter, aux[0]);
         iter_advance(q.dst, q.dstIter, (uint32_t)r - aux[1]);
         q.ret = r;
@@ -321,70 +405,74 @@ int LZ4E_compress_default(const struct bio_vec* src, struct bio_vec* dst, struct
     return r < 0 ? 0 : q.ret;
 }
 
+// Output staging a decode can need: a sequence of t input bytes writes at
+// most 19 + 255 t bytes (the literal/match varints, lz4e_decompress.c:194-220,
+// 316-336), so no input of csize bytes produces more than 263 * csize.  A
+// caller's capacity beyond that is never touched, and the kernel still sees
+// the caller's capacity (it steers the reference's bound checks).
+uint64_t decode_staging(int csize, int cap) {
+    if (cap <= 0) return 0;
+    const uint64_t most = 263ull * (uint64_t)std::max(csize, 0) + 64;
+    return std::min<uint64_t>((uint64_t)cap, most);
+}
+
 int lz4e_decompress_batch(const char* const* src, const int* csize, char* const* dst, const int* cap,
                           int* ret, int n) {
     if (n <= 0) return 0;
-    Ctx& c = ctx();
-    std::lock_guard<std::mutex> lk(c.mu);
     g_err.clear();
-    if (!c.init()) {
-        for (int i = 0; i < n; ++i) ret[i] = -1;
-        return -1;
-    }
+    for (int i = 0; i < n; ++i) ret[i] = -1;
+    if (!gate().check()) return -1;
     const uint32_t R = (uint32_t)n;
+    // [frames | descriptors | ret | outputs]
     std::vector<uint64_t> so(R), dso(R);
     uint64_t s = 0, d = 0;
     for (uint32_t i = 0; i < R; ++i) {
         so[i] = s;
         s += align16((uint64_t)std::max(csize[i], 0));
     }
+    const size_t m_so = s, m_sl = m_so + align16(8ull * R), m_do = m_sl + align16(4ull * R),
+                 m_dc = m_do + align16(8ull * R), m_rt = m_dc + align16(4ull * R),
+                 obase = m_rt + align16(4ull * R);
     for (uint32_t i = 0; i < R; ++i) {
-        dso[i] = s + d;
-        d += align16((uint64_t)std::max(cap[i], 0) + 64);
+        dso[i] = obase + d;
+        d += align16(decode_staging(csize[i], cap[i]) + 64);
     }
-    const size_t meta = align16(8ull * R) * 2 + align16(4ull * R) * 3;
-    if (!c.h_data.ensure(s + d) || !c.d_data.ensure(s + d) || !c.h_meta.ensure(meta) ||
-        !c.d_meta.ensure(meta)) {
-        for (int i = 0; i < n; ++i) ret[i] = -1;
-        return -1;
-    }
-    uint8_t* hd = static_cast<uint8_t*>(c.h_data.p);
-    uint8_t* hm = static_cast<uint8_t*>(c.h_meta.p);
-    const size_t m_so = 0, m_sl = align16(8ull * R), m_do = m_sl + align16(4ull * R),
-                 m_dc = m_do + align16(8ull * R), m_rt = m_dc + align16(4ull * R);
+    Lease ls;
+    if (!ls.acquire()) return -1;
+    CallCtx& c = *ls.c;
+    if (!c.grow(obase + d)) return -1;
+    uint8_t* hd = static_cast<uint8_t*>(c.h.p);
     for (uint32_t i = 0; i < R; ++i) {
         if (csize[i] > 0) std::memcpy(hd + so[i], src[i], (size_t)csize[i]);
-        reinterpret_cast<uint64_t*>(hm + m_so)[i] = so[i];
-        reinterpret_cast<int32_t*>(hm + m_sl)[i] = csize[i];
-        reinterpret_cast<uint64_t*>(hm + m_do)[i] = dso[i];
-        reinterpret_cast<int32_t*>(hm + m_dc)[i] = cap[i];
+        reinterpret_cast<uint64_t*>(hd + m_so)[i] = so[i];
+        reinterpret_cast<int32_t*>(hd + m_sl)[i] = csize[i];
+        reinterpret_cast<uint64_t*>(hd + m_do)[i] = dso[i];
+        reinterpret_cast<int32_t*>(hd + m_dc)[i] = cap[i];
     }
-    uint8_t* dd = static_cast<uint8_t*>(c.d_data.p);
-    uint8_t* dm = static_cast<uint8_t*>(c.d_meta.p);
-    bool ok = hip_ok(hipMemcpyAsync(dd, hd, s, hipMemcpyHostToDevice, c.stream), "H2D data") &&
-              hip_ok(hipMemcpyAsync(dm, hm, m_rt, hipMemcpyHostToDevice, c.stream), "H2D meta");
+    uint8_t* dd = static_cast<uint8_t*>(c.d.p);
+    const lz4e::DecompressBatch a{dd,
+                                  reinterpret_cast<const uint64_t*>(dd + m_so),
+                                  reinterpret_cast<const int32_t*>(dd + m_sl),
+                                  dd,
+                                  reinterpret_cast<const uint64_t*>(dd + m_do),
+                                  reinterpret_cast<const int32_t*>(dd + m_dc),
+                                  reinterpret_cast<int32_t*>(dd + m_rt),
+                                  R};
+    bool ok = hip_ok(hipMemcpyAsync(dd, hd, m_rt, hipMemcpyHostToDevice, c.stream), "H2D") &&
+              hip_ok(lz4e::launch_decompress(a, c.stream), "decompress launch") &&
+              hip_ok(copy_flat(c.h_dev, dd, m_rt, 4ull * R, c.stream), "copy-back ret");
     if (ok) {
-        lz4e::DecompressBatch a{dd,
-                                reinterpret_cast<const uint64_t*>(dm + m_so),
-                                reinterpret_cast<const int32_t*>(dm + m_sl),
-                                dd,
-                                reinterpret_cast<const uint64_t*>(dm + m_do),
-                                reinterpret_cast<const int32_t*>(dm + m_dc),
-                                reinterpret_cast<int32_t*>(dm + m_rt),
-                                R};
-        ok = hip_ok(lz4e::launch_decompress(a, c.stream), "decompress launch") &&
-             hip_ok(hipMemcpyAsync(hm + m_rt, dm + m_rt, 4ull * R, hipMemcpyDeviceToHost, c.stream),
-                    "D2H ret") &&
-             hip_ok(hipMemcpyAsync(hd + s, dd + s, d, hipMemcpyDeviceToHost, c.stream), "D2H data") &&
+        hipLaunchKernelGGL(copy_blocks_kernel, dim3(R), dim3(256), 0, c.stream, dd,
+                           static_cast<uint8_t*>(c.h_dev),
+                           reinterpret_cast<const uint64_t*>(dd + m_do),
+                           reinterpret_cast<const int32_t*>(dd + m_rt), R);
+        ok = hip_ok(hipGetLastError(), "copy-back data") &&
              hip_ok(hipStreamSynchronize(c.stream), "decompress sync");
     }
-    if (!ok) {
-        for (int i = 0; i < n; ++i) ret[i] = -1;
-        return -1;
-    }
+    if (!ok) return -1;
     int good = 0;
     for (uint32_t i = 0; i < R; ++i) {
-        ret[i] = reinterpret_cast<const int32_t*>(hm + m_rt)[i];
+        ret[i] = reinterpret_cast<const int32_t*>(hd + m_rt)[i];
         if (ret[i] >= 0) {
             if (ret[i] > 0) std::memcpy(dst[i], hd + dso[i], (size_t)ret[i]);
             good++;
@@ -411,11 +499,11 @@ int lz4e_decompress_sg_batch(const char* const* src, const int* csize, struct bi
     for (int i = 0; i < n; ++i) {
         cap[i] = (int)std::min<uint32_t>(dstIter[i]->bi_size, 0x7FFFFFFFu);
         at[i] = total;
-        total += (uint64_t)cap[i] + 1;
+        total += decode_staging(csize[i], cap[i]) + 1;
     }
-    std::vector<char> stage(total + 1);
+    std::unique_ptr<char[]> stage(new char[total + 1]);
     std::vector<char*> dp((size_t)n);
-    for (int i = 0; i < n; ++i) dp[i] = stage.data() + at[i];
+    for (int i = 0; i < n; ++i) dp[i] = stage.get() + at[i];
     const int good = lz4e_decompress_batch(src, csize, dp.data(), cap.data(), ret, n);
     if (good < 0) return -1;
     for (int i = 0; i < n; ++i) {
@@ -490,30 +578,6 @@ namespace {
 
 constexpr int kEIO = -5, kENOSPC = -28;
 
-// Device -> pinned host copy as a kernel on the slot's own stream.  The DMA
-// engine serves every stream's copies in submission order, so a D2H that
-// waits for its sub-batch's kernels would hold up the next sub-batch's H2D
-// (measured: the whole pipeline ran serialised).  Only H2D copies go to the
-// DMA engine; results come back through the host mapping of the pinned
-// buffer, 16 bytes per lane.
-__global__ __launch_bounds__(256) void copy_out_kernel(const uint4* __restrict__ src,
-                                                       uint4* __restrict__ dst, uint64_t n16) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride)
-        dst[i] = src[i];
-}
-
-// Copies bytes [off, off + n) of the slot's data buffer (16-B aligned offsets
-// and sizes) from HBM to the same offsets of its pinned twin.
-hipError_t copy_out(void* host_dev, const void* dev, uint64_t off, uint64_t n, hipStream_t st) {
-    if (n == 0) return hipSuccess;
-    const uint64_t n16 = (n + 15) / 16;
-    const uint32_t blocks = (uint32_t)std::min<uint64_t>(1024, (n16 + 255) / 256);
-    hipLaunchKernelGGL(copy_out_kernel, dim3(blocks), dim3(256), 0, st,
-                       reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(dev) + off),
-                       reinterpret_cast<uint4*>(static_cast<uint8_t*>(host_dev) + off), n16);
-    return hipGetLastError();
-}
 constexpr uint64_t kSubBytes = 64ull << 20;  // input bytes per pipeline sub-batch
 constexpr uint32_t kSubReqs = 16384;         // requests per sub-batch
 // Sub-batches in flight.  A sub-batch's kernels take about the slowest
@@ -611,7 +675,37 @@ struct ChunkProf {
     double wait = 0, out = 0, gather = 0, submit = 0;
 };
 
-bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chunk_stats* st,
+// vec_count of the bio the reference completes for one successful WRITE
+// (lz4e_bdev/lz4e_stats.c:47 adds bio->bi_vcnt): after the round trip the
+// request's bio is reset and re-pointed at the chunk's contiguous src buffer
+// (lz4e_req.c:191-197, lz4e_add_buf_to_bio :115-142), one bio_add_page per
+// page piece.  bio_add_page merges a piece into the previous bio_vec when it
+// starts where that one ends in memory (bvec_try_merge_page), which every
+// piece of a contiguous buffer does -- in this userspace model
+// page_address(p) == (char *)p, so contiguous virtual memory is contiguous
+// pages: the pieces after the first all merge.
+uint64_t bio_vcnt_of_buffer(const char* data, uint32_t len) {
+    uint64_t vcnt = 0;
+    const char* prev_end = nullptr;
+    uint32_t off = (uint32_t)(reinterpret_cast<uintptr_t>(data) & (LZ4E_PAGE_SIZE - 1));
+    uint32_t piece = std::min<uint32_t>(len, LZ4E_PAGE_SIZE - off);
+    while (len) {
+        if (data != prev_end) vcnt++;  // a new bio_vec unless it merges
+        prev_end = data + piece;
+        data += piece;
+        len -= piece;
+        piece = std::min<uint32_t>(len, LZ4E_PAGE_SIZE);
+    }
+    return vcnt;
+}
+
+// Debug hook (tests only, not part of include/lz4e.h): the pipeline fails
+// after this many sub-batches have been submitted (-1: never).
+std::atomic<int> g_chunk_fault_after{-1};
+
+// Waits for a slot's sub-batch and hands its results to the requests;
+// counts into `st` (this call's stats, added to the caller's on success).
+bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chunk_stats& st,
                   int& good, ChunkProf& pr) {
     if (!s.busy) return true;
     s.busy = false;
@@ -646,44 +740,72 @@ bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chu
     for (uint32_t j = 0; j < R; ++j) {
         const lz4e_chunk_request& q = reqs[s.req[j]];
         if (q.status == 0) good++;
-        if (st) {
-            st->reqs_total++;
-            if (q.status != 0) st->reqs_failed++;
-            else st->data_in_bytes += q.srcIter->bi_size;
-            st->frame_bytes += (uint64_t)q.comp_size;
+        st.reqs_total++;
+        if (q.status != 0) {
+            st.reqs_failed++;
+        } else {
+            st.data_in_bytes += q.srcIter->bi_size;
+            st.vec_count += bio_vcnt_of_buffer(q.data, q.srcIter->bi_size);
         }
+        st.frame_bytes += (uint64_t)q.comp_size;
     }
+    s.req.clear();
     return true;
+}
+
+// After a failure: wait out every slot still in flight (its kernels and
+// copies still target the slot's buffers) and forget its requests, so that
+// nothing of this call leaks into the next one.
+void chunk_drain(ChunkCtx& cc) {
+    for (uint32_t t = 0; t < kSlots; ++t) {
+        ChunkSlot& s = cc.slot[t];
+        if (s.busy) (void)hipEventSynchronize(s.done);
+        s.busy = false;
+        s.req.clear();
+    }
 }
 
 }  // namespace
 
 extern "C" {
 
+void lz4e_debug_chunk_fault_after(int subbatches) { g_chunk_fault_after.store(subbatches); }
+
 int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_chunk_stats* stats) {
     if (n <= 0) return 0;
-    for (int i = 0; i < n; ++i) {
-        reqs[i].comp_size = 0;
-        reqs[i].status = kEIO;
-    }
-    Ctx& c = ctx();
-    {
-        std::lock_guard<std::mutex> lk(c.mu);
-        g_err.clear();
-        if (!c.init()) return -1;
-    }
+    auto fail_all = [&]() {
+        for (int i = 0; i < n; ++i) {
+            reqs[i].comp_size = 0;
+            reqs[i].status = kEIO;
+        }
+        return -1;
+    };
+    fail_all();
+    g_err.clear();
+    if (!gate().check()) return -1;
     ChunkCtx& cc = chunk_ctx();
     std::lock_guard<std::mutex> lk(cc.mu);
     if (!cc.init()) return -1;
+    chunk_drain(cc);  // nothing of an earlier call may still be pending
 
+    struct lz4e_chunk_stats st = {0, 0, 0, 0, 0};
     int good = 0;
     uint32_t i = 0, k = 0;
     const uint32_t N = (uint32_t)n;
     ChunkProf pr;
     const double tstart = pr.on ? now_ms() : 0;
+    auto abort = [&]() {
+        chunk_drain(cc);
+        return fail_all();
+    };
     while (i < N) {
         ChunkSlot& s = cc.slot[k % kSlots];
-        if (!chunk_finish(s, reqs, stats, good, pr)) return -1;
+        if (!chunk_finish(s, reqs, st, good, pr)) return abort();
+        const int fa = g_chunk_fault_after.load();
+        if (fa >= 0 && k >= (uint32_t)fa) {
+            set_err("lz4e: injected pipeline fault");
+            return abort();
+        }
         // ---- form the sub-batch: requests [i, e) ----
         s.req.clear();
         s.fr.clear();
@@ -698,11 +820,11 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
             const uint32_t len = q.srcIter->bi_size;
             int t = LZ4E_TABLE_BYU16;
             if (len > LZ4E_MAX_INPUT_SIZE) {  // lz4e_compress.c:245-248 -> -EIO
-                if (stats) stats->reqs_total++, stats->reqs_failed++;
+                st.reqs_total++, st.reqs_failed++;
                 continue;
             }
             if (len >= 13 && (t = table_type_of(q.src, q.srcIter)) == 0) {  // :274-277
-                if (stats) stats->reqs_total++, stats->reqs_failed++;
+                st.reqs_total++, st.reqs_failed++;
                 continue;
             }
             s.req.push_back(i);
@@ -731,10 +853,10 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
         if (!s.h_data.ensure(total) || !s.d_data.ensure(total) || !s.h_meta.ensure(m.total) ||
             !s.d_meta.ensure(m.total) ||
             !hip_ok(hipHostGetDevicePointer(&s.h_dev, s.h_data.p, 0), "hipHostGetDevicePointer"))
-            return -1;
+            return abort();
         uint8_t* hd = static_cast<uint8_t*>(s.h_data.p);
         uint8_t* hm = static_cast<uint8_t*>(s.h_meta.p);
-        // ---- gather (overlaps the other slot's GPU work) ----
+        // ---- gather (overlaps the other slots' GPU work) ----
         const double tg = pr.on ? now_ms() : 0;
         par_for(R, ib, [&](uint32_t j) {
             const lz4e_chunk_request& q = reqs[s.req[j]];
@@ -756,9 +878,6 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
         s.meta_dret = m.dret;
         uint8_t* dd = static_cast<uint8_t*>(s.d_data.p);
         uint8_t* dm = static_cast<uint8_t*>(s.d_meta.p);
-        if (!hip_ok(hipMemcpyAsync(dd, hd, ib, hipMemcpyHostToDevice, s.stream), "H2D data") ||
-            !hip_ok(hipMemcpyAsync(dm, hm, m.ret, hipMemcpyHostToDevice, s.stream), "H2D meta"))
-            return -1;
         const lz4e::CompressBatch ca{dd,
                                      reinterpret_cast<const uint64_t*>(dm + m.in_off),
                                      reinterpret_cast<const uint32_t*>(dm + m.in_len),
@@ -779,24 +898,34 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
                                        reinterpret_cast<const int32_t*>(dm + m.out_cap),
                                        reinterpret_cast<int32_t*>(dm + m.dret),
                                        R};
-        if (!hip_ok(lz4e::launch_compress(ca, s.stream), "compress launch") ||
+        // from here on the slot has work in flight: a failure must drain it
+        s.busy = true;
+        if (!hip_ok(hipMemcpyAsync(dd, hd, ib, hipMemcpyHostToDevice, s.stream), "H2D data") ||
+            !hip_ok(hipMemcpyAsync(dm, hm, m.ret, hipMemcpyHostToDevice, s.stream), "H2D meta") ||
+            !hip_ok(lz4e::launch_compress(ca, s.stream), "compress launch") ||
             !hip_ok(lz4e::launch_decompress(da, s.stream), "decompress launch") ||
             !hip_ok(hipMemcpyAsync(hm + m.ret, dm + m.ret, m.total - m.ret, hipMemcpyDeviceToHost,
                                    s.stream), "D2H meta") ||
-            (frames && !hip_ok(copy_out(s.h_dev, dd, ib, fb, s.stream), "D2H frames")) ||
-            !hip_ok(copy_out(s.h_dev, dd, ib + fb, ob, s.stream), "D2H data") ||
+            (frames && !hip_ok(copy_flat(s.h_dev, dd, ib, fb, s.stream), "D2H frames")) ||
+            !hip_ok(copy_flat(s.h_dev, dd, ib + fb, ob, s.stream), "D2H data") ||
             !hip_ok(hipEventRecord(s.done, s.stream), "event record"))
-            return -1;
-        s.busy = true;
+            return abort();
         k++;
         if (pr.on) pr.submit += now_ms() - ts;
     }
     for (uint32_t t = 0; t < kSlots; ++t)
-        if (!chunk_finish(cc.slot[(k + t) % kSlots], reqs, stats, good, pr)) return -1;
+        if (!chunk_finish(cc.slot[(k + t) % kSlots], reqs, st, good, pr)) return abort();
     if (pr.on)
         fprintf(stderr, "lz4e chunk: %u sub-batches, total %.2f ms: gpu wait %.2f, copy-out %.2f, "
                 "gather %.2f, submit %.2f\n", k, now_ms() - tstart, pr.wait, pr.out, pr.gather,
                 pr.submit);
+    if (stats) {
+        stats->reqs_total += st.reqs_total;
+        stats->reqs_failed += st.reqs_failed;
+        stats->vec_count += st.vec_count;
+        stats->data_in_bytes += st.data_in_bytes;
+        stats->frame_bytes += st.frame_bytes;
+    }
     return good;
 }
 

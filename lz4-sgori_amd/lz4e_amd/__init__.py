@@ -88,7 +88,8 @@ class ChunkRequest(ctypes.Structure):
 class ChunkStats(ctypes.Structure):
     """struct lz4e_chunk_stats (include/lz4e.h)."""
     _fields_ = [("reqs_total", ctypes.c_uint64), ("reqs_failed", ctypes.c_uint64),
-                ("data_in_bytes", ctypes.c_uint64), ("frame_bytes", ctypes.c_uint64)]
+                ("vec_count", ctypes.c_uint64), ("data_in_bytes", ctypes.c_uint64),
+                ("frame_bytes", ctypes.c_uint64)]
 
 
 EIO, ENOSPC = 5, 28
@@ -368,6 +369,34 @@ def _ptr(t) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
+def _check_dev(n: int, **tensors) -> None:
+    """The kernels read raw pointers: every tensor must be contiguous, on one
+    HIP device, of the element type the C ABI expects, and (descriptors) hold
+    one entry per block -- a wrong dtype would be read as another width."""
+    import torch
+    want = {"src": torch.uint8, "dst": torch.uint8, "table_type": torch.uint8,
+            "src_off": torch.int64, "dst_off": torch.int64, "src_len": torch.int32,
+            "dst_cap": torch.int32, "ret": torch.int32, "aux": torch.int32}
+    per_block = {"src_off": 1, "dst_off": 1, "src_len": 1, "dst_cap": 1, "ret": 1,
+                 "table_type": 1, "aux": 2}
+    dev = None
+    for name, t in tensors.items():
+        if t is None:
+            continue
+        if t.dtype != want[name]:
+            raise TypeError(f"{name}: dtype {t.dtype}, expected {want[name]}")
+        if not t.is_cuda:
+            raise ValueError(f"{name}: not a device tensor")
+        if not t.is_contiguous():
+            raise ValueError(f"{name}: not contiguous")
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError(f"{name}: on {t.device}, other tensors on {dev}")
+        if name in per_block and t.numel() < per_block[name] * n:
+            raise ValueError(f"{name}: {t.numel()} entries for {n} blocks")
+
+
 def compress_batch_dev(src, src_off, src_len, table_type_, dst, dst_off, dst_cap, ret,
                        aux=None, max_len: Optional[int] = None, stream=None) -> None:
     """lz4e_compress_batch_dev on torch tensors (uint8 / int64 / int32 views).
@@ -378,6 +407,8 @@ def compress_batch_dev(src, src_off, src_len, table_type_, dst, dst_off, dst_cap
     """
     import torch  # local: the package itself does not need torch
     n = int(src_len.numel())
+    _check_dev(n, src=src, src_off=src_off, src_len=src_len, table_type=table_type_, dst=dst,
+               dst_off=dst_off, dst_cap=dst_cap, ret=ret, aux=aux)
     if max_len is None:
         max_len = int(src_len.max().item()) if n else 0
     if stream is None:
@@ -393,6 +424,9 @@ def decompress_batch_dev(src, src_off, src_len, dst, dst_off, dst_cap, ret, stre
     """lz4e_decompress_batch_dev on torch tensors (launch only)."""
     import torch
     n = int(src_len.numel())
+    # decompress descriptors: frame offsets int64, frame sizes / capacities / ret int32
+    _check_dev(n, src=src, src_off=src_off, src_len=src_len, dst=dst, dst_off=dst_off,
+               dst_cap=dst_cap, ret=ret)
     if stream is None:
         stream = torch.cuda.current_stream().cuda_stream
     r = lib().lz4e_decompress_batch_dev(_ptr(src), _ptr(src_off), _ptr(src_len), _ptr(dst),

@@ -47,6 +47,28 @@ def _jpeg() -> bytes:
     return bytes(np.random.default_rng(3).integers(0, 256, 275147, dtype=np.uint8))
 
 
+def _choice(rng, n: int, prob) -> np.ndarray:
+    """rng.choice(len(prob), size=n, p=prob), bit for bit, without its slow
+    binary search: the same uniforms (drawn in pieces: one stream), mapped
+    through a 2^16-bucket table of the CDF; only uniforms in a bucket that
+    straddles a CDF step take the search."""
+    cdf = np.cumsum(prob)
+    cdf /= cdf[-1]
+    K = 1 << 16
+    edges = np.arange(K + 1, dtype=np.float64) / K
+    ss = cdf.searchsorted(edges, side="right")
+    lo, hi = ss[:-1], ss[1:]
+    out = np.empty(n, dtype=np.int64)
+    for a in range(0, n, 1 << 24):
+        u = rng.random(min(1 << 24, n - a))
+        b = (u * K).astype(np.int64)
+        r = lo[b]
+        amb = lo[b] != hi[b]
+        r[amb] = cdf.searchsorted(u[amb], side="right")
+        out[a:a + u.size] = r
+    return out
+
+
 def text_proxy(nbytes: int, seed: int = 0x7E57) -> np.ndarray:
     """Word-level text from the lorem vocabulary, with sentence/line breaks."""
     rng = np.random.default_rng(seed)
@@ -54,13 +76,27 @@ def text_proxy(nbytes: int, seed: int = 0x7E57) -> np.ndarray:
     lens = np.array([len(w) + 1 for w in vocab])
     mean = float((lens * prob).sum())
     nwords = int(nbytes / mean * 1.05) + 16
-    idx = rng.choice(len(vocab), size=nwords, p=prob)
+    idx = _choice(rng, nwords, prob)
     # vocabulary bytes with a trailing separator; every ~12th separator a newline
-    table = [np.frombuffer(w + b" ", dtype=np.uint8) for w in vocab]
-    pieces = [table[i] for i in idx]
-    out = np.concatenate(pieces)
-    nl = rng.random(out.size) < (1.0 / (12 * mean))
-    out = np.where((out == 32) & nl, np.uint8(10), out).astype(np.uint8)
+    flat = np.frombuffer(b"".join(w + b" " for w in vocab), dtype=np.uint8)
+    start = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    wl = lens[idx]
+    out = np.empty(int(wl.sum()), dtype=np.uint8)
+    # gather the words in pieces (bounded temporaries), then the newlines:
+    # the same bytes and random stream as concatenating word by word
+    step, o = 1 << 22, 0
+    for a in range(0, nwords, step):
+        ii, ll = idx[a:a + step], wl[a:a + step]
+        tot = int(ll.sum())
+        first = np.cumsum(ll) - ll
+        pos = np.arange(tot, dtype=np.int64) + np.repeat(start[ii] - first, ll)
+        out[o:o + tot] = flat[pos]
+        o += tot
+    thr = 1.0 / (12 * mean)
+    for a in range(0, out.size, 1 << 26):
+        seg = out[a:a + (1 << 26)]
+        nl = rng.random(seg.size) < thr
+        seg[(seg == 32) & nl] = 10
     while out.size < nbytes:
         out = np.concatenate([out, text_proxy(nbytes - out.size, seed + 1)])
     return out[:nbytes]

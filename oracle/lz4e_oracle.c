@@ -480,7 +480,7 @@ err:
 /* ---------------------------------------------------------------------- */
 
 struct batch_job {
-	int kind; /* 0 compress, 1 decompress */
+	int kind; /* 0 compress, 1 decompress, 2 compress through bio_vecs */
 	const uint8_t *in;
 	const uint64_t *in_off;
 	const void *in_len;
@@ -491,7 +491,39 @@ struct batch_job {
 	int32_t *ret;
 	uint32_t n;
 	uint32_t next; /* atomic work counter */
+	uint32_t seg;  /* kind 2: source segment bytes */
 };
+
+/* One block of kind 2: the source as seg-byte bio_vecs, the destination as
+ * 4096-byte pages, through the faithful SG restatement (the reference's
+ * per-access segment walk, lz4e_defs.h:352-585). */
+static int32_t sg_block(const uint8_t *in, uint32_t n, uint32_t seg,
+			uint8_t *out, uint32_t cap)
+{
+	uint32_t ns = n ? (n + seg - 1) / seg : 1;
+	uint32_t nd = cap ? (cap + LZ4E_PAGE_SIZE - 1) / LZ4E_PAGE_SIZE : 1;
+	struct bio_vec *sv = calloc(ns + nd, sizeof(*sv));
+	struct bio_vec *dv = sv + ns;
+	struct bvec_iter si = { 0, n, 0, 0 }, di = { 0, cap, 0, 0 };
+	unsigned char wrk[LZ4E_MEM_COMPRESS];
+	uint32_t k;
+	int32_t r;
+
+	for (k = 0; k < ns; k++) {
+		sv[k].bv_page = (struct page *)(in + (size_t)k * seg);
+		sv[k].bv_len = n - k * seg < seg ? n - k * seg : seg;
+		sv[k].bv_offset = 0;
+	}
+	for (k = 0; k < nd; k++) {
+		dv[k].bv_page = (struct page *)(out + (size_t)k * LZ4E_PAGE_SIZE);
+		dv[k].bv_len = cap - k * LZ4E_PAGE_SIZE < LZ4E_PAGE_SIZE ?
+			cap - k * LZ4E_PAGE_SIZE : LZ4E_PAGE_SIZE;
+		dv[k].bv_offset = 0;
+	}
+	r = oracle_compress_sg(sv, dv, &si, &di, wrk);
+	free(sv);
+	return r;
+}
 
 static void *batch_worker(void *arg)
 {
@@ -502,7 +534,12 @@ static void *batch_worker(void *arg)
 
 		if (i >= j->n)
 			break;
-		if (j->kind == 0)
+		if (j->kind == 2)
+			j->ret[i] = sg_block(j->in + j->in_off[i],
+					     ((const uint32_t *)j->in_len)[i], j->seg,
+					     j->out + j->out_off[i],
+					     ((const uint32_t *)j->out_cap)[i]);
+		else if (j->kind == 0)
 			j->ret[i] = oracle_compress_linear(
 				j->in + j->in_off[i], ((const uint32_t *)j->in_len)[i],
 				j->ttype[i], j->out + j->out_off[i],
@@ -541,7 +578,19 @@ void oracle_compress_linear_batch(const uint8_t *in, const uint64_t *in_off,
 				  uint32_t n, int threads)
 {
 	struct batch_job j = { 0, in, in_off, in_len, ttype, out, out_off,
-			       out_cap, ret, n, 0 };
+			       out_cap, ret, n, 0, 0 };
+
+	run_batch(&j, threads);
+}
+
+void oracle_compress_sg_batch(const uint8_t *in, const uint64_t *in_off,
+			      const uint32_t *in_len, uint32_t seg,
+			      uint8_t *out, const uint64_t *out_off,
+			      const uint32_t *out_cap, int32_t *ret,
+			      uint32_t n, int threads)
+{
+	struct batch_job j = { 2, in, in_off, in_len, NULL, out, out_off,
+			       out_cap, ret, n, 0, seg };
 
 	run_batch(&j, threads);
 }
@@ -552,7 +601,7 @@ void oracle_decompress_batch(const uint8_t *in, const uint64_t *in_off,
 			     int32_t *ret, uint32_t n, int threads)
 {
 	struct batch_job j = { 1, in, in_off, in_len, NULL, out, out_off,
-			       out_cap, ret, n, 0 };
+			       out_cap, ret, n, 0, 0 };
 
 	run_batch(&j, threads);
 }

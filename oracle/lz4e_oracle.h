@@ -51,6 +51,13 @@ void oracle_compress_linear_batch(const uint8_t *in, const uint64_t *in_off,
 				  uint8_t *out, const uint64_t *out_off,
 				  const uint32_t *out_cap, int32_t *ret,
 				  uint32_t n, int threads);
+/* The same blocks through oracle_compress_sg: source split into seg-byte
+ * bio_vecs, destination 4096-byte pages (the reference's cost profile). */
+void oracle_compress_sg_batch(const uint8_t *in, const uint64_t *in_off,
+			      const uint32_t *in_len, uint32_t seg,
+			      uint8_t *out, const uint64_t *out_off,
+			      const uint32_t *out_cap, int32_t *ret,
+			      uint32_t n, int threads);
 void oracle_decompress_batch(const uint8_t *in, const uint64_t *in_off,
 			     const int32_t *in_len, uint8_t *out,
 			     const uint64_t *out_off, const int32_t *out_cap,

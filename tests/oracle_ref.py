@@ -41,6 +41,8 @@ def load():
     L.oracle_decompress_safe.restype = I32
     L.oracle_compress_linear_batch.argtypes = [P, P, P, P, P, P, P, P, U32, I32]
     L.oracle_compress_linear_batch.restype = None
+    L.oracle_compress_sg_batch.argtypes = [P, P, P, U32, P, P, P, P, U32, I32]
+    L.oracle_compress_sg_batch.restype = None
     L.oracle_decompress_batch.argtypes = [P, P, P, P, P, P, P, U32, I32]
     L.oracle_decompress_batch.restype = None
     _lib = L

@@ -44,11 +44,22 @@ def test_header_layouts(tmp_path):
         'int main(void){printf("%zu %zu %zu %zu %zu %zu %d\\n", sizeof(LZ4E_stream_t),'
         ' (size_t)LZ4E_MEM_COMPRESS, sizeof(struct bio_vec), sizeof(struct bvec_iter),'
         ' offsetof(struct bvec_iter, bi_size), offsetof(struct bio_vec, bv_offset),'
-        ' LZ4E_COMPRESSBOUND(65536)); return 0;}\n')
+        ' LZ4E_COMPRESSBOUND(65536));\n'
+        ' printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(struct lz4e_chunk_stats),'
+        ' offsetof(struct lz4e_chunk_stats, vec_count), offsetof(struct lz4e_chunk_stats, data_in_bytes),'
+        ' sizeof(struct lz4e_chunk_request), offsetof(struct lz4e_chunk_request, status),'
+        ' sizeof(struct lz4e_sg_request)); return 0;}\n')
     exe = tmp_path / "t"
     subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
     vals = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
-    s_stream, memc, s_bv, s_it, o_size, o_off, bound = map(int, vals)
+    s_stream, memc, s_bv, s_it, o_size, o_off, bound = map(int, vals[:7])
+    st_size, st_vec, st_data, rq_size, rq_status, sg_size = map(int, vals[7:])
+    assert st_size == ctypes.sizeof(lz4e_amd.ChunkStats)
+    assert st_vec == lz4e_amd.ChunkStats.vec_count.offset
+    assert st_data == lz4e_amd.ChunkStats.data_in_bytes.offset
+    assert rq_size == ctypes.sizeof(lz4e_amd.ChunkRequest)
+    assert rq_status == lz4e_amd.ChunkRequest.status.offset
+    assert sg_size == ctypes.sizeof(lz4e_amd.SgRequest)
     assert s_stream == memc == 17440
     assert s_bv == ctypes.sizeof(lz4e_amd.BioVec)
     assert s_it == ctypes.sizeof(lz4e_amd.BvecIter)

@@ -329,8 +329,11 @@ def test_full_size_roundtrip(gpu, cls, bs, kind):
 @pytest.mark.parametrize("cap_extra", [0, 100000])
 def test_decompress_periodic_matches(gpu, cap_extra):
     """Self-overlapping matches of every period 1..40 and lengths around
-    1x-3x the period (the overlap-copy cases), decoded through the LDS image
-    (capacity <= 64 KiB) and in HBM (larger capacity)."""
+    1x-3x the period (the overlap-copy cases).  With the exact capacity the
+    last sequences fall inside the reference's end-of-output margins
+    (op > oend - 32 / oend - 12: no shortcut, exact end checks,
+    lz4e_decompress.c:150-191, 223-288, 422-431); with 100 KB spare every
+    sequence stays on the fast path."""
     rng = np.random.default_rng(99)
     frames, caps, expect = [], [], []
     for period in range(1, 41):
@@ -370,6 +373,8 @@ def _chunk_check(gpu, srcs, payloads, want_frames=True):
             assert frame == ef
     assert good == len(srcs) - nfail
     assert stats.reqs_total == len(srcs) and stats.reqs_failed == nfail
+    # one merged bio_vec per successful non-empty request (lz4e_stats.c:47)
+    assert stats.vec_count == sum(1 for s, b in zip(srcs, payloads) if gpu.table_type(s) and len(b))
     assert stats.data_in_bytes == sum(len(b) for s, b in zip(srcs, payloads) if gpu.table_type(s))
     return stats
 
@@ -474,3 +479,139 @@ def test_decompress_safe_sg_single(gpu, test_files):
     assert d.it.bi_size == 0
     d2 = make_sg(b"", [4096] * 5, capacity=len(blk) - 1)
     assert gpu.decompress_safe_sg(ef, d2) == oracle_ref.decompress(ef, len(blk) - 1)[0] < 0
+
+
+def test_chunk_write_batch_fault_then_smaller_call(gpu):
+    """A pipeline failure part way through (injected after the first
+    sub-batch is in flight) returns -1 with every request -EIO and the
+    caller's stats untouched; the next, smaller call is unaffected by what
+    the failed one left in flight."""
+    bs, nreq = 65536, 1100  # two 64 MiB sub-batches
+    data = corpus.silesia_proxy(nreq * bs, 77)
+    srcs = [make_sg(data[i * bs:(i + 1) * bs].tobytes(), [4096] * 16) for i in range(nreq)]
+    L = gpu.lib()
+    L.lz4e_debug_chunk_fault_after.argtypes = [ctypes.c_int]
+    stats = gpu.ChunkStats()
+    L.lz4e_debug_chunk_fault_after(1)
+    try:
+        with pytest.raises(gpu.GpuUnavailable, match="injected"):
+            gpu.chunk_write_batch(srcs, want_frames=True, stats=stats)
+    finally:
+        L.lz4e_debug_chunk_fault_after(-1)
+    assert (stats.reqs_total, stats.reqs_failed, stats.vec_count, stats.data_in_bytes) == (0, 0, 0, 0)
+    small = srcs[:5]
+    good, res = gpu.chunk_write_batch(small, want_frames=True, stats=stats)
+    assert good == 5 and stats.reqs_total == 5 and stats.vec_count == 5
+    for i, (st, csize, d, fr) in enumerate(res):
+        blk = data[i * bs:(i + 1) * bs].tobytes()
+        er, ef, _, _ = oracle_ref.compress(blk, BYU16)
+        assert st == 0 and csize == er and d == blk and fr == ef
+
+
+def test_single_calls_concurrent(gpu, test_files):
+    """LZ4E_compress_default / LZ4E_decompress_safe from 8 threads at once
+    (the reference is reentrant given distinct wrkmem and is called from
+    every submitting CPU): every result equals the oracle's."""
+    import threading
+    rng = np.random.default_rng(5)
+    pool = _corpus("mixed", 1 << 20, 5).tobytes()
+    errors = []
+
+    def worker(t):
+        try:
+            for k in range(25):
+                n = int(rng.integers(0, 20000)) if k % 5 else 4096
+                s0 = int(rng.integers(0, len(pool) - n))
+                blk = pool[s0:s0 + n]
+                seg = [4096, 512][(t + k) % 2]
+                segs = [min(seg, n - j) for j in range(0, n, seg)] or [16]
+                src = make_sg(blk, segs, shuffle_seed=k)
+                cap = compress_bound(n)
+                dst = make_sg(b"", [4096] * (-(-cap // 4096) or 1), capacity=cap)
+                tt = gpu.table_type(src)
+                er, ef, fs, lr = oracle_ref.compress(blk, tt if n >= 13 else BYU16)
+                r = gpu.compress_default(src, dst)
+                if r != er or dst.read_prefix(r) != ef:
+                    errors.append(("compress", t, k, r, er))
+                    continue
+                d = gpu.decompress_safe(ef, n)
+                if d != (n, blk):
+                    errors.append(("decompress", t, k, d[0]))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append(("exception", t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:5]
+
+
+# ---------------------------------------------------------------------------
+# BASELINE configurations at full size: every frame and every decode
+# ---------------------------------------------------------------------------
+
+def _full_size(gpu, host, lens, bs, cls):
+    """Device-resident compress + decompress of equal-stride blocks, then
+    every frame against the oracle's and every decode against the input."""
+    import torch
+    n = len(lens)
+    lens = np.asarray(lens, dtype=np.int64)
+    offs = np.arange(n, dtype=np.int64) * bs
+    caps = lens + lens // 255 + 16
+    slot = (bs + bs // 255 + 16 + 64 + 15) // 16 * 16
+    doffs = np.arange(n, dtype=np.int64) * slot
+    dev = torch.device("cuda")
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).to(dev)
+    d_src = torch.from_numpy(host).to(dev)
+    d_dst = torch.zeros(n * slot, dtype=torch.uint8, device=dev)
+    ret = torch.zeros(n, dtype=torch.int32, device=dev)
+    gpu.compress_batch_dev(d_src, t(offs, np.int64), t(lens, np.int32), t(np.full(n, cls), np.uint8),
+                           d_dst, t(doffs, np.int64), t(caps, np.int32), ret, max_len=bs)
+    d_out = torch.zeros(n * bs + 64, dtype=torch.uint8, device=dev)
+    dret = torch.zeros(n, dtype=torch.int32, device=dev)
+    gpu.decompress_batch_dev(d_dst, t(doffs, np.int64), ret, d_out, t(offs, np.int64), t(lens, np.int32),
+                             dret)
+    torch.cuda.synchronize()
+    g_ret, g_dst = ret.cpu().numpy(), d_dst.cpu().numpy()
+    assert (dret.cpu().numpy() == lens).all()
+    U = int(lens.sum())
+    assert torch.equal(d_out[:U], d_src[:U])
+    del d_out, d_src
+    L = oracle_ref.load()
+    c_out = np.zeros(n * slot, np.uint8)
+    c_ret = np.zeros(n, np.int32)
+    L.oracle_compress_linear_batch(host.ctypes.data, offs.astype(np.uint64).ctypes.data,
+                                   lens.astype(np.uint32).ctypes.data, np.full(n, cls, np.uint8).ctypes.data,
+                                   c_out.ctypes.data, doffs.astype(np.uint64).ctypes.data,
+                                   caps.astype(np.uint32).ctypes.data, c_ret.ctypes.data, n, 16)
+    assert (g_ret == c_ret).all(), np.flatnonzero(g_ret != c_ret)[:10]
+    # every frame's bytes: mask the slots' tails and compare whole buffers
+    used = np.zeros(n * slot, dtype=bool).reshape(n, slot)
+    used[np.arange(slot)[None, :] < g_ret[:, None]] = True
+    used = used.reshape(-1)
+    bad = np.flatnonzero((g_dst != c_out) & used)
+    assert bad.size == 0, f"first differing frame {bad[0] // slot}"
+
+
+@pytest.mark.parametrize("name", ["silesia64k", "sg512", "fio4k", "text256k"])
+def test_full_size_every_frame(gpu, name):
+    """configs[1..4] at BASELINE's sizes: 3234 x 64 KiB byU16 (Silesia-proxy),
+    3234 x 64 KiB byU32 (the 128 x 512 B layout's class), 262144 x 4 KiB
+    (1 GiB fio pattern), 3815 x 256 KiB (10^9 B of text, last block
+    182,784 B)."""
+    bs, cls, n, total = {"silesia64k": (65536, BYU16, 3234, None), "sg512": (65536, BYU32, 3234, None),
+                         "fio4k": (4096, BYU16, 262144, None),
+                         "text256k": (262144, BYU32, 3815, 10**9)}[name]
+    total = total or n * bs
+    host = np.zeros(n * bs, np.uint8)
+    if name == "fio4k":
+        host[:total] = corpus.fio_pattern(total, 0xF10)
+    elif name == "text256k":
+        host[:total] = corpus.text_proxy(total, 0x7E57)
+    else:
+        host[:total] = corpus.silesia_proxy(total, 0x5157)
+    lens = np.full(n, bs, np.int64)
+    lens[-1] = total - (n - 1) * bs
+    _full_size(gpu, host, lens, bs, cls)

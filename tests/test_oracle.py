@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 
 import oracle_ref
-from lz4e_amd import BYU16, BYU32, compress_bound, make_sg
+from lz4e_amd import BYU16, BYU32, compress_bound, corpus, make_sg
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 KAT = json.load(open(os.path.join(GOLDEN, "reference_kat.json")))
@@ -193,3 +193,28 @@ def test_decompress_rejects_corruption():
     assert oracle_ref.decompress(bytes([0x00, 0x00, 0x00, 0x50]) + b"abcde", 100) == (9, b"\0" * 4 + b"abcde")
     # an offset reaching before the block start fails at ip = 3 (:299-302)
     assert oracle_ref.decompress(bytes([0x00, 0x01, 0x00, 0x50]) + b"abcde", 100)[0] == -4
+
+
+def test_sg_batch_equals_linear_batch():
+    """The CPU baseline's two variants (bench.py cpu_baseline / _sg) compute
+    the same frames: the faithful SG walk over 4 KiB and 512 B segments."""
+    L = oracle_ref.load()
+    nb, bs = 12, 65536
+    data = corpus.silesia_proxy(nb * bs, 9)
+    offs = np.arange(nb, dtype=np.uint64) * bs
+    lens = np.full(nb, bs, np.uint32)
+    cap = bs + bs // 255 + 16
+    caps = np.full(nb, cap, np.uint32)
+    slot = (cap + 64 + 15) // 16 * 16
+    doffs = np.arange(nb, dtype=np.uint64) * slot
+    for seg, tt in ((4096, 1), (512, 3)):
+        o1, r1 = np.zeros(nb * slot, np.uint8), np.zeros(nb, np.int32)
+        o2, r2 = np.zeros(nb * slot, np.uint8), np.zeros(nb, np.int32)
+        L.oracle_compress_linear_batch(data.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                       np.full(nb, tt, np.uint8).ctypes.data, o1.ctypes.data,
+                                       doffs.ctypes.data, caps.ctypes.data, r1.ctypes.data, nb, 4)
+        L.oracle_compress_sg_batch(data.ctypes.data, offs.ctypes.data, lens.ctypes.data, seg,
+                                   o2.ctypes.data, doffs.ctypes.data, caps.ctypes.data, r2.ctypes.data,
+                                   nb, 4)
+        assert (r1 == r2).all() and (r1 > 0).all()
+        assert np.array_equal(o1, o2)

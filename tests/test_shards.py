@@ -79,3 +79,122 @@ def test_two_rank_gloo_layout(tmp_path):
         assert (float(t0), float(t1)) == (1.5, 2.0)  # max over ranks
         stream[int(base):int(base) + len(local)] = local
     assert bytes(stream) == ref
+
+
+# ---------------------------------------------------------------------------
+# chunk queue + rebalance (north star: RCCL used only to rebalance the queue)
+# ---------------------------------------------------------------------------
+
+from lz4e_amd.shards import ChunkQueue, apply_moves, deal_chunks, rebalance_plan  # noqa: E402
+
+
+def test_deal_chunks_round_robin():
+    q = deal_chunks(10, 3)
+    assert q == [[0, 3, 6, 9], [1, 4, 7], [2, 5, 8]]
+    assert sorted(sum(q, [])) == list(range(10))
+
+
+def test_rebalance_plan_evens_projected_time():
+    queues = deal_chunks(40, 4)
+    nb = [16] * 40
+    busy = [4.0, 1.0, 1.0, 1.0]  # rank 0 four times slower per block
+    moves = rebalance_plan(queues, nb, busy)
+    assert moves and all(a == 0 for _, a, _ in moves)
+    q2 = apply_moves(queues, moves)
+    assert sorted(sum(q2, [])) == list(range(40))
+    rate = [10 * 16 / b for b in busy]
+    before = max(len(q) * 16 / r for q, r in zip(queues, rate))
+    after = max(len(q) * 16 / r for q, r in zip(q2, rate))
+    assert after < 0.5 * before
+    # balanced input: nothing moves; the plan is deterministic
+    assert rebalance_plan(queues, nb, [1.0] * 4) == []
+    assert rebalance_plan(queues, nb, busy) == moves
+
+
+def test_rebalance_plan_idle_rank():
+    # a rank with no chunks (more ranks than chunks) pulls work, never gives any
+    queues = deal_chunks(3, 4)
+    assert queues[3] == []
+    moves = rebalance_plan(queues, [16, 16, 16], [1.0, 1.0, 1.0, 0.0])
+    assert all(b != 3 or a != 3 for _, a, b in moves)
+
+
+def _rebalance_worker(rank, world, port, n_blocks, chunk, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle_ref
+    bs = 4096
+    q = ChunkQueue(n_blocks, chunk, rank, world)
+    data = corpus.silesia_proxy(n_blocks * bs, 0x5157, chunk=bs)
+    held = {}
+    for c in q.queue:  # only this rank's initial chunks are materialised here
+        lo, hi = q.chunk_range(c)
+        held[c] = torch.from_numpy(data[lo * bs:hi * bs].copy())
+    del data
+    # calibration: rank 0 reports itself 3x slower per block -> it gives chunks away
+    nb = len(q.blocks())
+    stats = q.progress(nb, 0, (3.0 if rank == 0 else 1.0) * nb, dist.group.WORLD)
+    moves = q.rebalance(stats, held, lambda c: (q.chunk_range(c)[1] - q.chunk_range(c)[0]) * bs,
+                        dist.group.WORLD)
+    assert sorted(held) == sorted(q.queue)
+    frames = {}
+    for c in q.queue:
+        lo, hi = q.chunk_range(c)
+        buf = held[c].numpy()
+        for k, blk in enumerate(range(lo, hi)):
+            frames[blk] = oracle_ref.compress(buf[k * bs:(k + 1) * bs].tobytes(), BYU16)[1]
+    with open(os.path.join(out_dir, f"q{rank}.txt"), "w") as f:
+        f.write(" ".join(f"{b}:{len(frames[b])}" for b in sorted(frames)) + "\n")
+        f.write(" ".join(f"{c},{a},{b}" for c, a, b in moves))
+    with open(os.path.join(out_dir, f"q{rank}.bin"), "wb") as f:
+        f.write(b"".join(frames[b] for b in sorted(frames)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_rebalance(tmp_path):
+    """The calibrated rebalance moves chunks (payload over point-to-point
+    send/recv) and the job's frames, reassembled in block order, equal the
+    single-process stream."""
+    import oracle_ref
+    world, n, chunk = 2, 45, 4
+    mp.spawn(_rebalance_worker, args=(world, _free_port(), n, chunk, str(tmp_path)), nprocs=world,
+             join=True)
+    frames = {}
+    moves_seen = []
+    for r in range(world):
+        head, mv = open(tmp_path / f"q{r}.txt").read().split("\n")
+        blob = open(tmp_path / f"q{r}.bin", "rb").read()
+        pos = 0
+        for tok in head.split():
+            b, ln = map(int, tok.split(":"))
+            assert b not in frames
+            frames[b] = blob[pos:pos + ln]
+            pos += ln
+        moves_seen.append(mv)
+    assert moves_seen[0] == moves_seen[1] and moves_seen[0]  # same plan everywhere, non-empty
+    assert all(m.split(",")[1] == "0" for m in moves_seen[0].split())
+    assert sorted(frames) == list(range(n))
+    data = corpus.silesia_proxy(n * 4096, 0x5157, chunk=4096)
+    ref = [oracle_ref.compress(data[i * 4096:(i + 1) * 4096].tobytes(), BYU16)[1] for i in range(n)]
+    assert [frames[i] for i in range(n)] == ref
+
+
+def test_bench_launches_ranks():
+    """bench.py --gpus 2 starts two ranks itself (launcher check, no GPU)."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, timeout=180, env=env, check=True).stdout
+    line = [x for x in out.splitlines() if x.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 2 and sorted(r["rank"] for r in res["ranks"]) == [0, 1]
+    env["WORLD_SIZE"] = "3"
+    bad = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, timeout=60, env=env)
+    assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr

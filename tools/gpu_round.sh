@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU session: smoke -> parity tests -> bench.  Stops at the first step
-# that faults, aborts, times out or hangs (exit codes other than 0/1).
+# that faults, aborts, times out or hangs (any exit code other than 0/1).
+#   tools/gpu_round.sh [pytest -k expression]
 mkdir -p gpurun_out
 step() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
@@ -12,6 +13,7 @@ step() {  # name timeout cmd...
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)" >&2; exit $rc; fi
   return 0
 }
-step smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 900 python -m pytest tests -m gpu -q -rf --timeout 300
-step bench 600 python bench.py --steps 3 --warmup 1
+K=${1:+-k "$1"}
+step smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread $K
+step bench 600 python -u bench.py --steps 10 --warmup 3
