@@ -141,6 +141,7 @@ class Batch:
         nblk = len(lens)
         self.nblk, self.bs, self.cls, self.dev, self.lens = nblk, bs, cls, dev, lens
         self.U = int(lens.sum())
+        self.max_cap = int(lens.max()) if nblk else 0
         self.offs = np.arange(nblk, dtype=np.int64) * bs
         self.cap1 = bs + bs // 255 + 16
         self.slot = (self.cap1 + 64 + 15) // 16 * 16
@@ -166,7 +167,8 @@ class Batch:
     def decompress(self):
         import lz4e_amd
         lz4e_amd.decompress_batch_dev(self.d_dst, self.d_doff, self.d_ret, self.d_out, self.d_off,
-                                      self.d_len, self.d_dret, stream=self.stream.cuda_stream)
+                                      self.d_len, self.d_dret, stream=self.stream.cuda_stream,
+                                      max_cap=self.max_cap)
 
     def run(self, steps: int, timed: bool):
         """steps x (compress, decompress); -> (wall s, mean compress ms, mean decompress ms)."""

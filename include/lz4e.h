@@ -196,13 +196,17 @@ int lz4e_compress_batch_dev(const uint8_t *src, const uint64_t *src_off,
 /*
  * Device-resident batch decompress.  Block i decodes src_len[i] bytes at
  * src + src_off[i] into at most dst_cap[i] bytes at dst + dst_off[i];
- * ret[i] receives LZ4E_decompress_safe's return value.
+ * ret[i] receives LZ4E_decompress_safe's return value.  `max_cap` bounds
+ * dst_cap[] (0 = unknown): up to 65536 selects the workgroup decoder (the
+ * block's output image in LDS), otherwise one wave decodes each block.
+ * Both return identical values and bytes.
  * Returns 0 on a successful launch, else a negative error.
  */
 int lz4e_decompress_batch_dev(const uint8_t *src, const uint64_t *src_off,
 			      const int32_t *src_len, uint8_t *dst,
 			      const uint64_t *dst_off, const int32_t *dst_cap,
-			      int32_t *ret, uint32_t nblocks, void *stream);
+			      int32_t *ret, uint32_t nblocks, uint32_t max_cap,
+			      void *stream);
 
 /*
  * LZ4E_decompress_safe into a bio_vec list (the read

@@ -40,6 +40,7 @@
 // + jump table 4,224 B = 7,744 B.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 
 #include "lz4e_device.h"
@@ -847,9 +848,511 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
                           (lu16*)(smem + kRing + kRingPad + kSink + kSpan));
 }
 
+// ============================================================================
+// Workgroup decoder: one block per 256-thread workgroup, output image in LDS
+// ============================================================================
+//
+// For blocks whose capacity is at most 64 KiB (the 4 KiB and 64 KiB chunk
+// sizes).  The one-wave decoder above is bound by its serial chain: one
+// batch of <= 64 sequences at a time, and dependent short matches (records,
+// integer tables) resolved a few bytes per lane per round.  Here the four
+// waves of a workgroup share the block:
+//
+//  1. Parse, a 1 KiB window of the token stream per batch.  Every window
+//     position is parsed speculatively as if a token started there (its next
+//     token position J1, extension bytes included); the true tokens are the
+//     orbit of the window's first position, found by pointer doubling over
+//     J (J2 = J1 o J1, ...) with the marking rule
+//     mark(J_{2^k}(p)) |= mark(p): after 9 levels every chain element of
+//     index < 512 (> the 342 tokens a 1 KiB window can hold) is marked.
+//     A workgroup scan over the marks gives each token its rank and output
+//     position.
+//  2. Check, per token, every bound the reference tests on its path
+//     (lz4e_decompress.c:123-446: the two-stage shortcut's entry
+//     conditions, literal end margins, extension-byte limits, offset inside
+//     the output, match end margin, the exact final literal run).  A block
+//     with any token that fails them -- malformed input, a too-small
+//     capacity -- is decoded from scratch by the one-wave exact decoder
+//     above (wave 0), so return values and error codes are the reference's
+//     by construction.  Blocks that pass produce the reference's bytes: its
+//     copies implement plain LZ semantics (offset 0 writes zeros).
+//  3. Literals: per sequence, long runs by the whole workgroup.
+//  4. Matches, in output sub-spans of 2 KiB: every byte finds its sequence
+//     (scatter of sequence starts + max scan), a byte whose source lies
+//     before the sub-span (self-overlap folded: out[m + t] =
+//     out[m - off + t mod off]) or in a literal is final at once; the rest
+//     point at their source byte and resolve by pointer jumping (a chain of
+//     depth d in log2 d rounds).
+//  5. The finished image leaves LDS in 16-byte stores.
+constexpr uint32_t kWgT = 256;                  // threads per workgroup (4 waves)
+constexpr uint32_t kWgWaves = kWgT / kWave;
+constexpr uint32_t kWin = 1024;                 // token-stream bytes parsed per batch
+constexpr uint32_t kWinPad = 256;               // staged bytes past the window
+constexpr uint32_t kMaxSeq = kWin / 3 + 2;      // a non-final sequence takes >= 3 input bytes
+constexpr uint32_t kSub = 2048;                 // output bytes resolved per sub-span
+constexpr uint32_t kOutMax = 65536;             // largest capacity this decoder takes
+constexpr uint32_t kLevels = 9;                 // 2^9 > kMaxSeq
+constexpr uint16_t kNone = 0xFFFF;              // no target / final byte
+constexpr uint32_t kLongLit = 64;               // longer literal runs: whole workgroup
+constexpr uint32_t kMaxLong = 32;
+constexpr uint32_t kLenCap = 1u << 20;          // speculative lengths saturate here
+
+struct WgLds {
+    uint8_t out[kOutMax + 16];
+    uint8_t win[kWin + kWinPad + 16];
+    union {
+        struct {
+            uint16_t a[kWin], b[kWin];  // J_{2^k}, J_{2^{k+1}} (window offsets)
+        } j;
+        uint16_t ptr[kSub];  // sub-span: sequence id + 1, then source byte / kNone
+    } u;
+    uint8_t mark[kWin];
+    uint32_t s_op[kMaxSeq], s_lit[kMaxSeq], s_len[kMaxSeq], s_off[kMaxSeq], s_m4[kMaxSeq];
+    uint32_t red[4 * kWgWaves];
+    uint32_t longs[kMaxLong];
+    int32_t st[8];
+};
+static_assert(sizeof(WgLds) <= 81920, "two workgroups per CU");
+static_assert(kRing + kRingPad + kSink + kSpan + kJump <= kOutMax, "fallback LDS inside the image");
+
+typedef __attribute__((address_space(1))) const uint8_t gcu8;
+typedef __attribute__((address_space(1))) const u32a1 gcu32a1;
+
+// The staged window [ip0, ip0 + kWin + kWinPad) from LDS, anything else from
+// HBM (zero past the input, like the staging).
+struct WinSrc {
+    const uint8_t* win;
+    gcu8* in;
+    int32_t n, ip0;
+    LZ4E_DEV uint32_t at(int32_t q) const {
+        const uint32_t r = (uint32_t)(q - ip0);
+        if (r < kWin + kWinPad) return win[r];
+        return q < n ? in[q] : 0u;
+    }
+};
+
+// One sequence read as if a token started at t (lz4e_decompress.c:123-336
+// field layout): literal start/length, offset, position after the match
+// length's extension bytes (the next token), match length + MINMATCH.
+struct Tok {
+    uint32_t token, lit, len, off, xm, m4;
+};
+
+LZ4E_DEV Tok parse_tok(const WinSrc& S, int32_t t) {
+    Tok k;
+    k.token = S.at(t);
+    uint32_t L = k.token >> 4, M = k.token & 15;
+    int32_t x = t + 1;
+    if (L == 15) {
+        uint32_t s;
+        do {
+            s = S.at(x++);
+            L += s;
+        } while (s == 255 && x < S.n && L < kLenCap);
+    }
+    k.lit = (uint32_t)x;
+    k.len = L;
+    x += (int32_t)L;
+    k.off = S.at(x) | (S.at(x + 1) << 8);
+    x += 2;
+    if (M == 15) {
+        uint32_t s;
+        do {
+            s = S.at(x++);
+            M += s;
+        } while (s == 255 && x < S.n && M < kLenCap);
+    }
+    k.xm = (uint32_t)x;
+    k.m4 = M + 4;
+    return k;
+}
+
+// Next-token offset of window position r if a token started there, or kNone
+// when that lies at or past the window end (only the staged bytes are read:
+// anything longer leaves the window anyway).
+LZ4E_DEV uint16_t jump1(const uint8_t* win, uint32_t r) {
+    const uint32_t tok = win[r];
+    uint32_t L = tok >> 4, x = r + 1;
+    if (L == 15) {
+        uint32_t s;
+        do {
+            s = win[x++];
+            L += s;
+        } while (s == 255 && x < kWin);
+    }
+    x += L + 2;
+    if (x >= kWin) return kNone;
+    if ((tok & 15) == 15) {
+        uint32_t s;
+        do {
+            s = win[x++];
+        } while (s == 255 && x < kWin);
+    }
+    return x < kWin ? (uint16_t)x : kNone;
+}
+
+// Exclusive workgroup prefix sums of two values; totals through t0 / t1.
+LZ4E_DEV void wg_scan2(uint32_t v0, uint32_t v1, uint32_t* red, uint32_t tid, uint32_t& e0,
+                       uint32_t& e1, uint32_t& t0, uint32_t& t1) {
+    const uint32_t i0 = wave_incl_add(v0), i1 = wave_incl_add(v1);
+    const uint32_t w = tid / kWave;
+    if (tid % kWave == kWave - 1) {
+        red[w] = i0;
+        red[kWgWaves + w] = i1;
+    }
+    __syncthreads();
+    uint32_t b0 = 0, b1 = 0, s0 = 0, s1 = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kWgWaves; ++i) {
+        const uint32_t r0 = red[i], r1 = red[kWgWaves + i];
+        if (i < w) b0 += r0, b1 += r1;
+        s0 += r0, s1 += r1;
+    }
+    __syncthreads();
+    e0 = b0 + i0 - v0;
+    e1 = b1 + i1 - v1;
+    t0 = s0;
+    t1 = s1;
+}
+
+// Exclusive workgroup prefix max of values >= 0 (0 for the first thread).
+LZ4E_DEV int32_t wg_excl_max(int32_t v, uint32_t* red, uint32_t tid) {
+    const int32_t ex = wave_excl_max(v);  // lane 0: INT32_MIN
+    const int32_t in = ex > v ? ex : v;
+    const uint32_t w = tid / kWave;
+    if (tid % kWave == kWave - 1) red[2 * kWgWaves + w] = (uint32_t)in;
+    __syncthreads();
+    int32_t b = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kWgWaves; ++i)
+        if (i < w) b = b > (int32_t)red[2 * kWgWaves + i] ? b : (int32_t)red[2 * kWgWaves + i];
+    __syncthreads();
+    return b > ex ? b : ex;
+}
+
+// len literal bytes at lit into the image at o (one thread).
+LZ4E_DEV void lit_copy(uint8_t* out, uint32_t o, const WinSrc& S, uint32_t lit, uint32_t len) {
+    const uint32_t r = lit - (uint32_t)S.ip0;
+    uint8_t* d = out + o;
+    uint32_t k = 0;
+    if (r + len <= kWin + kWinPad) {
+        const uint8_t* s = S.win + r;
+        for (; k + 4 <= len; k += 4) st4((lu8*)(d + k), ld4((const lu8*)(s + k)));
+        for (; k < len; ++k) d[k] = s[k];
+    } else {
+        gcu8* s = S.in + lit;
+        for (; k + 4 <= len; k += 4) st4((lu8*)(d + k), *(gcu32a1*)(s + k));
+        for (; k < len; ++k) d[k] = s[k];
+    }
+}
+
+// The one-wave exact decoder on wave 0 (reference bound checks and error
+// codes), LDS carved from the image.
+LZ4E_DEV void wg_fallback(WgLds& L, const uint8_t* in, int32_t srcSize, uint8_t* gout,
+                          int32_t outSize, int32_t* ret_slot, uint32_t tid) {
+    if (tid >= kWave) return;
+    uint8_t* smem = L.out;
+    decode_block<false>(in, srcSize, gout, outSize, ret_slot, nullptr, tid,
+                        (lu8*)(smem + kRing + kRingPad + kSink), (lu32*)smem,
+                        (lu16*)(smem + kRing + kRingPad + kSink + kSpan));
+}
+
+__global__ __launch_bounds__(kWgT) void decompress_wg_kernel(const uint8_t* __restrict__ src,
+                                                             const uint64_t* __restrict__ src_off,
+                                                             const int32_t* __restrict__ src_len,
+                                                             uint8_t* dst,
+                                                             const uint64_t* __restrict__ dst_off,
+                                                             const int32_t* __restrict__ dst_cap,
+                                                             int32_t* __restrict__ ret,
+                                                             uint32_t nblocks) {
+    __shared__ __attribute__((aligned(16))) WgLds L;
+    const uint32_t b = blockIdx.x;
+    if (b >= nblocks) return;
+    const uint32_t tid = threadIdx.x;
+    const int32_t srcSize = src_len[b];
+    const int32_t outSize = dst_cap[b];
+    const uint8_t* in = src + src_off[b];
+    uint8_t* gout = dst + dst_off[b];
+    if (special_case(in, srcSize, outSize, ret + b, tid)) return;
+    if (outSize > (int32_t)kOutMax) {
+        wg_fallback(L, in, srcSize, gout, outSize, ret + b, tid);
+        return;
+    }
+    const int32_t iend = srcSize, oend = outSize;
+    int32_t ip0 = 0, op = 0;
+    bool fallback = false, done = false;
+
+    while (!done) {
+        // ---- stage the window, speculative next-token table --------------
+        for (uint32_t i = tid; i < kWin + kWinPad; i += kWgT) {
+            const int32_t q = ip0 + (int32_t)i;
+            L.win[i] = q < srcSize ? in[q] : 0;
+        }
+        if (tid == 0) L.st[5] = 0;  // long literal runs of this batch
+        __syncthreads();
+        const WinSrc S{L.win, (gcu8*)in, srcSize, ip0};
+#pragma unroll
+        for (uint32_t k = 0; k < kWin / kWgT; ++k) {
+            const uint32_t r = tid + k * kWgT;
+            L.u.j.a[r] = ip0 + (int32_t)r < srcSize ? jump1(L.win, r) : kNone;
+            L.mark[r] = r == 0;
+        }
+        __syncthreads();
+        // ---- the true token chain: doubling + marking --------------------
+        {
+            uint16_t* A = L.u.j.a;
+            uint16_t* B = L.u.j.b;
+            for (uint32_t lev = 0; lev < kLevels; ++lev) {
+                uint16_t nb[kWin / kWgT];
+#pragma unroll
+                for (uint32_t k = 0; k < kWin / kWgT; ++k) {
+                    const uint32_t r = tid + k * kWgT;
+                    const uint16_t a = A[r];
+                    nb[k] = kNone;
+                    if (a != kNone) {
+                        if (L.mark[r]) L.mark[a] = 1;  // racy reads only add true tokens
+                        nb[k] = A[a];
+                    }
+                }
+                __syncthreads();
+                if (lev + 1 < kLevels) {
+#pragma unroll
+                    for (uint32_t k = 0; k < kWin / kWgT; ++k) B[tid + k * kWgT] = nb[k];
+                    __syncthreads();
+                    uint16_t* t = A;
+                    A = B;
+                    B = t;
+                }
+            }
+        }
+        // ---- tokens: rank, output position, the reference's checks --------
+        const uint32_t mk = *reinterpret_cast<const uint32_t*>(&L.mark[4 * tid]);
+        Tok tk[4];
+        uint32_t cnt = 0, osz = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            if ((mk >> (8 * q)) & 0xFF) {
+                tk[q] = parse_tok(S, ip0 + (int32_t)(4 * tid + q));
+                const bool fin = (int64_t)tk[q].lit + tk[q].len == iend;
+                cnt++;
+                osz += tk[q].len + (fin ? 0u : tk[q].m4);
+                if (osz > kLenCap) osz = kLenCap;  // malformed: caught by the checks
+            }
+        }
+        uint32_t rank, obase, nseq, osum;
+        wg_scan2(cnt, osz, L.red, tid, rank, obase, nseq, osum);
+        bool bad = false, fin_here = false;
+        int32_t o = op + (int32_t)obase;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            if (!((mk >> (8 * q)) & 0xFF)) continue;
+            const Tok& k = tk[q];
+            const int32_t t = ip0 + (int32_t)(4 * tid + q);
+            const uint32_t Lnib = k.token >> 4, Mnib = k.token & 15;
+            const int64_t litEnd = (int64_t)k.lit + k.len;
+            const bool fin = litEnd == iend;
+            // the two-stage shortcut's entry (:150-155)
+            const bool sc = Lnib != 15 && t + 1 < iend - 16 && o <= oend - 32;
+            // literal-length varint read exactly as the reference's bounded loop (:194-220)
+            const bool lext = Lnib != 15 || (int64_t)k.lit <= (int64_t)iend - 15;
+            bool ok;
+            if (fin) {
+                // final literal run (:223-288): not on the shortcut, fits the output
+                ok = !sc && lext && (int64_t)o + k.len <= oend;
+                fin_here = true;
+            } else {
+                const int64_t mo = (int64_t)o + k.len;  // match start
+                // _copy_match (:298-336, :422-431): offset inside the output,
+                // extension bytes before iend - 5, match end before oend - 5
+                const bool cm = (int64_t)k.off <= mo &&
+                                (Mnib != 15 || (int64_t)k.xm <= (int64_t)iend - 5) &&
+                                mo + k.m4 <= (int64_t)oend - 5;
+                if (sc) ok = (Mnib != 15 && k.off >= 8 && (int64_t)k.off <= mo) || cm;
+                else ok = lext && mo <= (int64_t)oend - 12 && litEnd <= (int64_t)iend - 8 && cm;
+                ok = ok && (int64_t)k.xm < iend;  // the next token exists
+            }
+            bad |= !ok;
+            if (rank < kMaxSeq) {
+                L.s_op[rank] = (uint32_t)o;
+                L.s_lit[rank] = k.lit;
+                L.s_len[rank] = k.len;
+                L.s_off[rank] = k.off;
+                L.s_m4[rank] = fin ? 0u : k.m4;
+                if (k.len > kLongLit) {
+                    const uint32_t li = atomicAdd((uint32_t*)&L.st[5], 1u);
+                    if (li < kMaxLong) L.longs[li] = rank;
+                    else bad = true;
+                }
+            } else {
+                bad = true;
+            }
+            if (rank + 1 == nseq) {  // the batch's last token: where the next batch starts
+                L.st[0] = (int32_t)k.xm;
+                L.st[1] = fin;
+            }
+            o += (int32_t)(k.len + (fin ? 0u : k.m4));
+            rank++;
+        }
+        bad = __syncthreads_or(bad ? 1 : 0) != 0 || nseq == 0;
+        const bool any_fin = __syncthreads_or(fin_here ? 1 : 0) != 0;
+        if (bad || (any_fin && !L.st[1])) {
+            fallback = true;
+            break;
+        }
+        const int32_t op_b = op, op_e = op + (int32_t)osum;
+        const int32_t next_ip = L.st[0];
+        const uint32_t nlong = (uint32_t)L.st[5];
+
+        // ---- literals ------------------------------------------------------
+        for (uint32_t i = tid; i < nseq; i += kWgT) {
+            const uint32_t len = L.s_len[i];
+            if (len > 0 && len <= kLongLit) lit_copy(L.out, L.s_op[i], S, L.s_lit[i], len);
+        }
+        for (uint32_t li = 0; li < nlong; ++li) {
+            const uint32_t i = L.longs[li];
+            const uint32_t len = L.s_len[i], o0 = L.s_op[i], lit = L.s_lit[i];
+            for (uint32_t k = 4 * tid; k < len; k += 4 * kWgT) {
+                const uint32_t c = len - k < 4 ? len - k : 4;
+                lit_copy(L.out, o0 + k, S, lit + k, c);
+            }
+        }
+        __syncthreads();
+
+        // ---- matches, 2 KiB sub-spans -----------------------------------------
+        for (int32_t a = op_b; a < op_e; a += (int32_t)kSub) {
+            const int32_t span = op_e - a < (int32_t)kSub ? op_e - a : (int32_t)kSub;
+            for (uint32_t j = tid; j < kSub; j += kWgT) L.u.ptr[j] = 0;
+            __syncthreads();
+            if (tid == 0) {
+                // the sequence covering a: last one starting at or before it
+                uint32_t lo = 0, hi = nseq - 1;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi + 1) / 2;
+                    if ((int32_t)L.s_op[mid] <= a) lo = mid;
+                    else hi = mid - 1;
+                }
+                L.u.ptr[0] = (uint16_t)(lo + 1);
+            }
+            for (uint32_t i = tid; i < nseq; i += kWgT) {
+                const int32_t so = (int32_t)L.s_op[i];
+                if (so > a && so < a + span) L.u.ptr[so - a] = (uint16_t)(i + 1);
+            }
+            __syncthreads();
+            // byte j = kPer tid + q of the sub-span: its sequence (max scan)
+            constexpr uint32_t kPer = kSub / kWgT;
+            int32_t sid[kPer];
+            int32_t run = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < kPer; ++q) {
+                const int32_t v = L.u.ptr[kPer * tid + q];
+                run = run > v ? run : v;
+                sid[q] = run;
+            }
+            const int32_t pre = wg_excl_max(run, L.red, tid);
+            uint16_t pv[kPer];
+            uint32_t pend = 0;  // my bytes still pointing at an unresolved source
+            uint32_t cs = 0xFFFFFFFFu, c_o = 0, c_len = 0, c_off = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < kPer; ++q) {
+                const int32_t s1 = sid[q] > pre ? sid[q] : pre;
+                const int32_t j = (int32_t)(kPer * tid + q);
+                const int32_t x = a + j;
+                pv[q] = kNone;
+                if (j >= span || s1 == 0) continue;
+                const uint32_t s = (uint32_t)s1 - 1;
+                if (s != cs) {
+                    cs = s;
+                    c_o = L.s_op[s];
+                    c_len = L.s_len[s];
+                    c_off = L.s_off[s];
+                }
+                const int32_t m = (int32_t)(c_o + c_len);
+                if (x < m) continue;  // literal: copied above
+                if (c_off == 0) {     // offset 0 writes zeros (:313, 407-415)
+                    L.out[x] = 0;
+                    continue;
+                }
+                // out[m + t] = out[m - off + t mod off]: the source is before the match
+                const uint32_t t = (uint32_t)(x - m);
+                const int32_t srcp = (t >= c_off) ? m - (int32_t)c_off + (int32_t)(t % c_off)
+                                                  : x - (int32_t)c_off;
+                if (srcp < a) {
+                    L.out[x] = L.out[srcp];  // final: every byte before the sub-span is
+                } else {
+                    pv[q] = (uint16_t)(srcp - a);
+                    pend |= 1u << q;
+                }
+            }
+            __syncthreads();  // every sequence id read before the pointers overwrite them
+#pragma unroll
+            for (uint32_t q = 0; q < kPer; ++q) L.u.ptr[kPer * tid + q] = pv[q];
+            // pointer jumping: a byte whose source is final copies it, the
+            // others jump to their source's source
+            while (__syncthreads_or(pend != 0)) {
+                uint8_t val[kPer];
+                uint32_t got = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < kPer; ++q) {
+                    val[q] = 0;
+                    if (!((pend >> q) & 1)) continue;
+                    const uint16_t py = L.u.ptr[pv[q]];
+                    if (py == kNone) {
+                        val[q] = L.out[a + pv[q]];
+                        got |= 1u << q;
+                    } else {
+                        pv[q] = py;
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (uint32_t q = 0; q < kPer; ++q) {
+                    if (!((pend >> q) & 1)) continue;
+                    const uint32_t j = kPer * tid + q;
+                    if ((got >> q) & 1) {
+                        L.out[a + j] = val[q];
+                        L.u.ptr[j] = kNone;
+                    } else {
+                        L.u.ptr[j] = pv[q];
+                    }
+                }
+                pend &= ~got;
+            }
+        }
+        op = op_e;
+        ip0 = next_ip;
+        done = any_fin;
+        __syncthreads();
+    }
+    if (fallback) {
+        __syncthreads();
+        wg_fallback(L, in, srcSize, gout, outSize, ret + b, tid);
+        return;
+    }
+    // ---- the image to HBM: 16-byte stores ---------------------------------
+    typedef __attribute__((address_space(1))) uint8_t gu8b;
+    const uint32_t head = (uint32_t)((16 - (reinterpret_cast<uintptr_t>(gout) & 15)) & 15);
+    const uint32_t n = (uint32_t)op;
+    const uint32_t h = head < n ? head : n;
+    for (uint32_t i = tid; i < h; i += kWgT) ((gu8b*)gout)[i] = L.out[i];
+    const uint32_t body = (n - h) & ~15u;
+    for (uint32_t c = h + 16 * tid; c < h + body; c += 16 * kWgT) {
+        const lu8* s = (const lu8*)(L.out + c);
+        stg16(gout + c, make_uint4(ld4(s), ld4(s + 4), ld4(s + 8), ld4(s + 12)));
+    }
+    for (uint32_t i = h + body + tid; i < n; i += kWgT) ((gu8b*)gout)[i] = L.out[i];
+    if (tid == 0) ret[b] = op;
+}
+
 template <bool kStamps>
 hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* dbg) {
     if (a.nblocks == 0) return hipSuccess;
+    // LZ4E_DECOMPRESS_WAVE=1 keeps every block on the one-wave decoder (A/B).
+    static const bool wave_only = getenv("LZ4E_DECOMPRESS_WAVE") != nullptr;
+    if (!kStamps && !wave_only && a.max_cap > 0 && a.max_cap <= kOutMax) {
+        hipLaunchKernelGGL(decompress_wg_kernel, dim3(a.nblocks), dim3(kWgT), 0, stream, a.src,
+                           a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((decompress_kernel<kStamps>), dim3(a.nblocks), dim3(kWave), 0, stream,
                        a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
                        dbg);

@@ -35,6 +35,9 @@ struct DecompressBatch {
     const int32_t* dst_cap;
     int32_t* ret;
     uint32_t nblocks;
+    // Upper bound of dst_cap[] (0: unknown).  At most 64 KiB selects the
+    // workgroup decoder (output image in LDS); otherwise one wave per block.
+    uint32_t max_cap;
 };
 
 uint32_t compress_lds_bytes(uint32_t max_len, bool lds_input);

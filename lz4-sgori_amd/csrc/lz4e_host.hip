@@ -457,7 +457,8 @@ int lz4e_decompress_batch(const char* const* src, const int* csize, char* const*
                                   reinterpret_cast<const uint64_t*>(dd + m_do),
                                   reinterpret_cast<const int32_t*>(dd + m_dc),
                                   reinterpret_cast<int32_t*>(dd + m_rt),
-                                  R};
+                                  R,
+                                  (uint32_t)std::max(0, *std::max_element(cap, cap + n))};
     bool ok = hip_ok(hipMemcpyAsync(dd, hd, m_rt, hipMemcpyHostToDevice, c.stream), "H2D") &&
               hip_ok(lz4e::launch_decompress(a, c.stream), "decompress launch") &&
               hip_ok(copy_flat(c.h_dev, dd, m_rt, 4ull * R, c.stream), "copy-back ret");
@@ -552,7 +553,7 @@ int lz4e_debug_compress_stamped(const uint8_t* src, const uint64_t* src_off, con
 int lz4e_debug_decompress_stamped(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
                                   uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
                                   int32_t* ret, uint32_t nblocks, void* stream, uint64_t* dbg) {
-    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks};
+    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, 0};
     return hip_ok(lz4e::launch_decompress_stamped(a, static_cast<hipStream_t>(stream), dbg),
                   "decompress launch")
                ? 0
@@ -561,9 +562,9 @@ int lz4e_debug_decompress_stamped(const uint8_t* src, const uint64_t* src_off, c
 
 int lz4e_decompress_batch_dev(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
                               uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
-                              int32_t* ret, uint32_t nblocks, void* stream) {
+                              int32_t* ret, uint32_t nblocks, uint32_t max_cap, void* stream) {
     g_err.clear();
-    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks};
+    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap};
     return hip_ok(lz4e::launch_decompress(a, static_cast<hipStream_t>(stream)), "decompress launch")
                ? 0
                : -1;
@@ -897,7 +898,8 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
                                        reinterpret_cast<const uint64_t*>(dm + m.out_off),
                                        reinterpret_cast<const int32_t*>(dm + m.out_cap),
                                        reinterpret_cast<int32_t*>(dm + m.dret),
-                                       R};
+                                       R,
+                                       max_len};
         // from here on the slot has work in flight: a failure must drain it
         s.busy = true;
         if (!hip_ok(hipMemcpyAsync(dd, hd, ib, hipMemcpyHostToDevice, s.stream), "H2D data") ||

@@ -132,7 +132,7 @@ def lib() -> ctypes.CDLL:
     L.lz4e_decompress_batch.restype = I32
     L.lz4e_compress_batch_dev.argtypes = [P, P, P, P, P, P, P, P, P, U32, U32, P]
     L.lz4e_compress_batch_dev.restype = I32
-    L.lz4e_decompress_batch_dev.argtypes = [P, P, P, P, P, P, P, U32, P]
+    L.lz4e_decompress_batch_dev.argtypes = [P, P, P, P, P, P, P, U32, U32, P]
     L.lz4e_decompress_batch_dev.restype = I32
     L.lz4e_chunk_write_batch.argtypes = [ctypes.POINTER(ChunkRequest), I32, ctypes.POINTER(ChunkStats)]
     L.lz4e_chunk_write_batch.restype = I32
@@ -420,16 +420,23 @@ def compress_batch_dev(src, src_off, src_len, table_type_, dst, dst_off, dst_cap
         raise RuntimeError("lz4e_compress_batch_dev: " + last_error())
 
 
-def decompress_batch_dev(src, src_off, src_len, dst, dst_off, dst_cap, ret, stream=None) -> None:
-    """lz4e_decompress_batch_dev on torch tensors (launch only)."""
+def decompress_batch_dev(src, src_off, src_len, dst, dst_off, dst_cap, ret, stream=None,
+                         max_cap: Optional[int] = None) -> None:
+    """lz4e_decompress_batch_dev on torch tensors (launch only).
+
+    ``max_cap`` bounds dst_cap (default: read from it, which synchronises);
+    up to 65536 selects the workgroup decoder."""
     import torch
     n = int(src_len.numel())
+    if max_cap is None:
+        max_cap = int(dst_cap.max().item()) if n else 0
     # decompress descriptors: frame offsets int64, frame sizes / capacities / ret int32
     _check_dev(n, src=src, src_off=src_off, src_len=src_len, dst=dst, dst_off=dst_off,
                dst_cap=dst_cap, ret=ret)
     if stream is None:
         stream = torch.cuda.current_stream().cuda_stream
     r = lib().lz4e_decompress_batch_dev(_ptr(src), _ptr(src_off), _ptr(src_len), _ptr(dst),
-                                        _ptr(dst_off), _ptr(dst_cap), _ptr(ret), n, stream)
+                                        _ptr(dst_off), _ptr(dst_cap), _ptr(ret), n,
+                                        max(0, int(max_cap)), stream)
     if r != 0:
         raise RuntimeError("lz4e_decompress_batch_dev: " + last_error())

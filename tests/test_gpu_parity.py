@@ -72,7 +72,7 @@ def _gpu_compress(amd, blocks, ttypes, caps=None):
     return r, frames, ax
 
 
-def _gpu_decompress(amd, frames, caps, csizes=None):
+def _gpu_decompress(amd, frames, caps, csizes=None, max_cap=None):
     import torch
     n = len(frames)
     csizes = [len(f) for f in frames] if csizes is None else csizes
@@ -92,7 +92,7 @@ def _gpu_decompress(amd, frames, caps, csizes=None):
     dst = torch.zeros(int(doffs[-1] + slot[-1]) + 16, dtype=torch.uint8, device=dev)
     ret = torch.full((n,), -7777, dtype=torch.int32, device=dev)
     amd.decompress_batch_dev(src, t(offs, np.int64), t(csizes, np.int32), dst, t(doffs, np.int64),
-                             t(caps, np.int32), ret)
+                             t(caps, np.int32), ret, max_cap=max_cap)
     torch.cuda.synchronize()
     r = ret.cpu().numpy()
     d = dst.cpu().numpy()
@@ -582,10 +582,12 @@ def _full_size(gpu, host, lens, bs, cls):
     L = oracle_ref.load()
     c_out = np.zeros(n * slot, np.uint8)
     c_ret = np.zeros(n, np.int32)
-    L.oracle_compress_linear_batch(host.ctypes.data, offs.astype(np.uint64).ctypes.data,
-                                   lens.astype(np.uint32).ctypes.data, np.full(n, cls, np.uint8).ctypes.data,
-                                   c_out.ctypes.data, doffs.astype(np.uint64).ctypes.data,
-                                   caps.astype(np.uint32).ctypes.data, c_ret.ctypes.data, n, 16)
+    # named arrays: a temporary's buffer could be freed before the C call reads it
+    a_off, a_len = offs.astype(np.uint64), lens.astype(np.uint32)
+    a_tt, a_doff, a_cap = np.full(n, cls, np.uint8), doffs.astype(np.uint64), caps.astype(np.uint32)
+    L.oracle_compress_linear_batch(host.ctypes.data, a_off.ctypes.data, a_len.ctypes.data,
+                                   a_tt.ctypes.data, c_out.ctypes.data, a_doff.ctypes.data,
+                                   a_cap.ctypes.data, c_ret.ctypes.data, n, 16)
     assert (g_ret == c_ret).all(), np.flatnonzero(g_ret != c_ret)[:10]
     # every frame's bytes: mask the slots' tails and compare whole buffers
     used = np.zeros(n * slot, dtype=bool).reshape(n, slot)
@@ -615,3 +617,42 @@ def test_full_size_every_frame(gpu, name):
     lens = np.full(n, bs, np.int64)
     lens[-1] = total - (n - 1) * bs
     _full_size(gpu, host, lens, bs, cls)
+
+
+@pytest.mark.parametrize("kind", ["mixed", "text", "runs", "ints", "random", "small_alpha", "fio"])
+def test_decompress_workgroup_vs_wave_decoder(gpu, kind):
+    """The two decoders on the same frames -- the workgroup decoder (LDS image,
+    max_cap <= 64 KiB) and the one-wave decoder (max_cap = 0) -- valid frames,
+    exact and spare capacities, and corrupted ones (the workgroup decoder's
+    checks hand those to the exact path): identical values and bytes, both
+    equal to the oracle's."""
+    rng = np.random.default_rng(zlib.crc32(kind.encode()))
+    data = _corpus(kind, 1 << 20, 31)
+    frames, caps, want = [], [], []
+    for i in range(48):
+        n = int(rng.choice([0, 1, 13, 100, 4096, 20000, 65536, int(rng.integers(1, 65537))]))
+        s0 = int(rng.integers(0, data.size - n + 1))
+        blk = data[s0:s0 + n].tobytes()
+        f = oracle_ref.compress(blk, BYU16)[1]
+        mode = i % 6
+        cap = n
+        if mode == 1:
+            cap = min(65536, n + int(rng.integers(1, 200)))
+        elif mode == 2 and len(f) > 2:
+            f = f[:int(rng.integers(1, len(f)))]
+        elif mode == 3 and len(f) > 0:
+            fb = bytearray(f)
+            for _ in range(3):
+                fb[int(rng.integers(0, len(fb)))] ^= 1 << int(rng.integers(0, 8))
+            f = bytes(fb)
+        elif mode == 4:
+            cap = max(0, n - int(rng.integers(1, 64)))
+        frames.append(f)
+        caps.append(cap)
+        want.append(oracle_ref.decompress(f, cap))
+    r_wg, o_wg = _gpu_decompress(gpu, frames, caps, max_cap=65536)
+    r_wv, o_wv = _gpu_decompress(gpu, frames, caps, max_cap=0)
+    for i, (er, eb) in enumerate(want):
+        assert r_wg[i] == er == r_wv[i], (i, r_wg[i], er, r_wv[i])
+        if er >= 0:
+            assert o_wg[i] == eb == o_wv[i], i

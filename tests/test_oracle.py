@@ -210,8 +210,9 @@ def test_sg_batch_equals_linear_batch():
     for seg, tt in ((4096, 1), (512, 3)):
         o1, r1 = np.zeros(nb * slot, np.uint8), np.zeros(nb, np.int32)
         o2, r2 = np.zeros(nb * slot, np.uint8), np.zeros(nb, np.int32)
+        tts = np.full(nb, tt, np.uint8)
         L.oracle_compress_linear_batch(data.ctypes.data, offs.ctypes.data, lens.ctypes.data,
-                                       np.full(nb, tt, np.uint8).ctypes.data, o1.ctypes.data,
+                                       tts.ctypes.data, o1.ctypes.data,
                                        doffs.ctypes.data, caps.ctypes.data, r1.ctypes.data, nb, 4)
         L.oracle_compress_sg_batch(data.ctypes.data, offs.ctypes.data, lens.ctypes.data, seg,
                                    o2.ctypes.data, doffs.ctypes.data, caps.ctypes.data, r2.ctypes.data,
