@@ -1057,6 +1057,20 @@ LZ4E_DEV void wg_fallback(WgLds& L, const uint8_t* in, int32_t srcSize, uint8_t*
                         (lu16*)(smem + kRing + kRingPad + kSink + kSpan));
 }
 
+// Phase cycle counters of the diagnostic build (tid 0's clock; phases are
+// separated by workgroup barriers): stage+J1, doubling, tokens, literals,
+// matches, flush, batches, sub-span rounds.
+struct WgStamps {
+    uint64_t t = 0, acc[6] = {0, 0, 0, 0, 0, 0}, batches = 0, rounds = 0;
+    LZ4E_DEV void lap(bool on, int ph) {
+        if (!on) return;
+        const uint64_t now = clock64();
+        acc[ph] += now - t;
+        t = now;
+    }
+};
+
+template <bool kStamps>
 __global__ __launch_bounds__(kWgT) void decompress_wg_kernel(const uint8_t* __restrict__ src,
                                                              const uint64_t* __restrict__ src_off,
                                                              const int32_t* __restrict__ src_len,
@@ -1064,8 +1078,12 @@ __global__ __launch_bounds__(kWgT) void decompress_wg_kernel(const uint8_t* __re
                                                              const uint64_t* __restrict__ dst_off,
                                                              const int32_t* __restrict__ dst_cap,
                                                              int32_t* __restrict__ ret,
-                                                             uint32_t nblocks) {
+                                                             uint32_t nblocks,
+                                                             uint64_t* __restrict__ dbg) {
     __shared__ __attribute__((aligned(16))) WgLds L;
+    WgStamps stp;
+    const bool on = kStamps && threadIdx.x == 0;
+    if (on) stp.t = clock64();
     const uint32_t b = blockIdx.x;
     if (b >= nblocks) return;
     const uint32_t tid = threadIdx.x;
@@ -1098,6 +1116,8 @@ __global__ __launch_bounds__(kWgT) void decompress_wg_kernel(const uint8_t* __re
             L.mark[r] = r == 0;
         }
         __syncthreads();
+        stp.lap(on, 0);
+        if (on) stp.batches++;
         // ---- the true token chain: doubling + marking --------------------
         {
             uint16_t* A = L.u.j.a;
@@ -1125,6 +1145,7 @@ __global__ __launch_bounds__(kWgT) void decompress_wg_kernel(const uint8_t* __re
                 }
             }
         }
+        stp.lap(on, 1);
         // ---- tokens: rank, output position, the reference's checks --------
         const uint32_t mk = *reinterpret_cast<const uint32_t*>(&L.mark[4 * tid]);
         Tok tk[4];
@@ -1199,6 +1220,7 @@ __global__ __launch_bounds__(kWgT) void decompress_wg_kernel(const uint8_t* __re
             fallback = true;
             break;
         }
+        stp.lap(on, 2);
         const int32_t op_b = op, op_e = op + (int32_t)osum;
         const int32_t next_ip = L.st[0];
         const uint32_t nlong = (uint32_t)L.st[5];
@@ -1217,6 +1239,7 @@ __global__ __launch_bounds__(kWgT) void decompress_wg_kernel(const uint8_t* __re
             }
         }
         __syncthreads();
+        stp.lap(on, 3);
 
         // ---- matches, 2 KiB sub-spans -----------------------------------------
         for (int32_t a = op_b; a < op_e; a += (int32_t)kSub) {
@@ -1316,8 +1339,10 @@ __global__ __launch_bounds__(kWgT) void decompress_wg_kernel(const uint8_t* __re
                     }
                 }
                 pend &= ~got;
+                if (on) stp.rounds++;
             }
         }
+        stp.lap(on, 4);
         op = op_e;
         ip0 = next_ip;
         done = any_fin;
@@ -1341,6 +1366,16 @@ __global__ __launch_bounds__(kWgT) void decompress_wg_kernel(const uint8_t* __re
     }
     for (uint32_t i = h + body + tid; i < n; i += kWgT) ((gu8b*)gout)[i] = L.out[i];
     if (tid == 0) ret[b] = op;
+    if (kStamps) {
+        __syncthreads();
+        stp.lap(on, 5);
+        if (on && dbg) {
+            uint64_t* d = dbg + 8 * (size_t)b;
+            for (int i = 0; i < 6; ++i) d[i] = stp.acc[i];
+            d[6] = stp.batches;
+            d[7] = stp.rounds;
+        }
+    }
 }
 
 template <bool kStamps>
@@ -1348,9 +1383,10 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
     if (a.nblocks == 0) return hipSuccess;
     // LZ4E_DECOMPRESS_WAVE=1 keeps every block on the one-wave decoder (A/B).
     static const bool wave_only = getenv("LZ4E_DECOMPRESS_WAVE") != nullptr;
-    if (!kStamps && !wave_only && a.max_cap > 0 && a.max_cap <= kOutMax) {
-        hipLaunchKernelGGL(decompress_wg_kernel, dim3(a.nblocks), dim3(kWgT), 0, stream, a.src,
-                           a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks);
+    if (!wave_only && a.max_cap > 0 && a.max_cap <= kOutMax) {
+        hipLaunchKernelGGL((decompress_wg_kernel<kStamps>), dim3(a.nblocks), dim3(kWgT), 0, stream,
+                           a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret,
+                           a.nblocks, dbg);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((decompress_kernel<kStamps>), dim3(a.nblocks), dim3(kWave), 0, stream,

@@ -549,11 +549,13 @@ int lz4e_debug_compress_stamped(const uint8_t* src, const uint64_t* src_off, con
 }
 
 // Diagnostic (not part of include/lz4e.h): the decompress kernel with
-// per-block phase cycle counters, 8 x u64 per block into dbg.
+// per-block phase cycle counters, 8 x u64 per block into dbg (max_cap as in
+// lz4e_decompress_batch_dev: <= 64 KiB stamps the workgroup decoder).
 int lz4e_debug_decompress_stamped(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
                                   uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
-                                  int32_t* ret, uint32_t nblocks, void* stream, uint64_t* dbg) {
-    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, 0};
+                                  int32_t* ret, uint32_t nblocks, void* stream, uint64_t* dbg,
+                                  uint32_t max_cap) {
+    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap};
     return hip_ok(lz4e::launch_decompress_stamped(a, static_cast<hipStream_t>(stream), dbg),
                   "decompress launch")
                ? 0
