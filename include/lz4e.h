@@ -197,9 +197,10 @@ int lz4e_compress_batch_dev(const uint8_t *src, const uint64_t *src_off,
  * Device-resident batch decompress.  Block i decodes src_len[i] bytes at
  * src + src_off[i] into at most dst_cap[i] bytes at dst + dst_off[i];
  * ret[i] receives LZ4E_decompress_safe's return value.  `max_cap` bounds
- * dst_cap[] (0 = unknown): up to 65536 selects the workgroup decoder (the
- * block's output image in LDS), otherwise one wave decodes each block.
- * Both return identical values and bytes.
+ * dst_cap[] (0 = unknown): 16 KiB and more (or unknown) selects the
+ * pipelined decoder (one parser wave and three copier waves per block),
+ * smaller blocks decode on one wave each.  Both return identical values and
+ * bytes.
  * Returns 0 on a successful launch, else a negative error.
  */
 int lz4e_decompress_batch_dev(const uint8_t *src, const uint64_t *src_off,

@@ -1,43 +1,40 @@
-// lz4e_decompress.hip -- gfx950 LZ4E safe block decoder.
+// lz4e_decompress.hip -- gfx950 LZ4E safe block decoders.
 //
 // Restates /root/reference/lz4e/lz4e_decompress.c:62-469
 // (LZ4E_decompress_generic, instance endOnInputSize + decode_full_block +
-// noDict) on one wave64 per block, in batches of up to 64 sequences:
+// noDict).  Both decoders share one parse (parse_batch) and differ in how the
+// copies of a batch are scheduled:
 //
-//  1. Parse: the token stream is walked wave-uniformly (scalar registers)
-//     with the reference's exact sequence of bound checks -- including the
-//     two-stage 16/18-byte shortcut, whose entry conditions change which
-//     malformed inputs are rejected and where -- so the return value,
-//     including the error code -(ip - src) - 1, is the reference's.  The
-//     compressed bytes come from two 256-byte register windows read with
-//     v_readlane (a third is prefetched one segment ahead).  Sequence k of
-//     the batch is recorded in lane k (literal source, literal length,
-//     output position, offset, match length).  Errors depend only on the
-//     token stream, so a failing block stops here.
-//  2. Literals: every lane copies its own run; runs longer than kLong are
-//     copied by the whole wave.
-//  3. Matches, in dependency rounds: a match is ready once the part of its
-//     source before its own output overlaps no earlier match of the batch
-//     that is still pending (checked exactly against each pending interval).
-//     Ready short matches are copied per lane, every load before any store;
-//     long ones by the whole wave in lane order.  Overlapping matches follow LZ semantics
-//     out[op + t] = out[op - off + t mod off]; offset 0 writes zeros, which
-//     is what the reference's LZ4_write32(op, offset) + overlap copy produce
-//     (lz4e_decompress.c:313, 407-415).
+//  * Parse, in batches of up to 64 sequences: the token stream is walked
+//    wave-uniformly with the reference's exact sequence of bound checks --
+//    including the two-stage 16/18-byte shortcut, whose entry conditions
+//    change which malformed inputs are rejected and where -- so the return
+//    value, including the error code -(ip - src) - 1, is the reference's.  A
+//    fast batch (no extension bytes, far from both block ends) is found by
+//    pointer doubling over a 256-byte window of the token stream; anything
+//    else is one sequence on the exact scalar path.  Sequence k of a batch is
+//    recorded in lane k (literal source, literal length, output position,
+//    offset, match length).
+//  * decompress_kernel, one wave per block (blocks under 16 KiB): the wave
+//    parses a batch, then copies it -- fast batches assembled in a small LDS
+//    span (literals from a 1 KiB LDS ring that mirrors the compressed
+//    segments the parse loaded, match sources before the batch from HBM,
+//    in-batch dependencies in rounds or by pointer jumping over the span's
+//    bytes) and written with one pass of 16-byte stores; scalar-path batches
+//    (long runs, block ends) copy in HBM.  LDS per block: ring 1 KiB +
+//    mirror 128 B + store sink 256 B + span 2,112 B + jump table 4,224 B =
+//    7,744 B.
+//  * decompress_pipe_kernel, one 4-wave workgroup per block (16 KiB and up):
+//    wave 0 parses while three copier waves assemble three batches at once,
+//    cross-batch sources resolved from the spans of the two previous batches
+//    (see the section below).  19 KiB of LDS per block.
 //
-// Output placement: every block decodes in place in its HBM destination.
-// A fast batch (no extension bytes, far from both block ends) is first
-// assembled in a small LDS span -- literals from a 1 KiB LDS ring that
-// mirrors the compressed segments the parse loaded, the part of each match
-// source before the batch from HBM in one round trip, the rest in LDS
-// dependency rounds or, for chains of dependent matches, by pointer jumping
-// over the span's bytes -- and written to HBM with one pass of 16-byte
-// stores.  Scalar-path batches (long runs, block ends) copy in HBM directly;
-// same-wave stores and loads to one global address are ordered by the
-// hardware (one vector L1 per CU), and wavefront-scope fences keep the
+// Overlapping matches follow LZ semantics out[op + t] = out[op - off + t]
+// byte by byte; offset 0 writes zeros, which is what the reference's
+// LZ4_write32(op, offset) + overlap copy produce (lz4e_decompress.c:313,
+// 407-415).  Same-wave stores and loads to one global address are ordered by
+// the hardware (one vector L1 per CU), and wavefront-scope fences keep the
 // compiler from moving a phase's loads above the previous phase's stores.
-// LDS per block: ring 1 KiB + mirror 128 B + store sink 256 B + span 2,112 B
-// + jump table 4,224 B = 7,744 B.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -470,12 +467,242 @@ LZ4E_DEV uint32_t table_compose(uint32_t A, uint32_t B) {
     return r;
 }
 
+
+// ---------------------------------------------------------------- the parse
+
+// Parse state of one block: wave-uniform scalars plus the input window.
+struct Parse {
+    InWindow win;
+    int32_t iend, oend, shortiend, shortoend;
+    int32_t ip, op;
+    bool done;  // the final literal run has been parsed
+
+    LZ4E_DEV void init(const uint8_t* in, int32_t srcSize, int32_t outSize, lu32* ring,
+                       uint32_t lane) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(in);
+        win.shift = (int32_t)(a & 3);
+        win.w = (gcu32*)(a - win.shift);
+        win.last = (srcSize + win.shift - 1) >> 2;
+        win.lane = lane;
+        win.ring = ring;
+        win.reload(0);
+        iend = srcSize;
+        oend = outSize;
+        shortiend = iend - 14 - 2;  // :100-101
+        shortoend = oend - 14 - 18; // :102-103
+        ip = 0;
+        op = 0;
+        done = false;
+    }
+};
+
+// One parsed batch: lane k < n holds sequence k (literal source, literal
+// length, output position, offset, match length; the final literal run has
+// match length 0).
+struct Batch {
+    int32_t ls = 0, L = 0, op = 0, off = 0, M = 0;
+    uint32_t n = 0;
+};
+
+enum ParseResult { kParsedFast, kParsedScalar, kParseFail };
+
+// The next batch of the token stream, with every bound check of the
+// reference in its order (lz4e_decompress.c:123-446).  kParsedFast: up to 64
+// sequences without extension bytes, far from both block ends (each literal
+// run <= 14, match length <= 18, output <= 32 bytes per sequence);
+// kParsedScalar: one sequence of any length; kParseFail: malformed input or
+// too small a capacity, the return value is -(P.ip) - 1.  A fast batch's
+// output is at most cap_out (>= 32) bytes.
+LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_out = 64 * 32) {
+    const int32_t iend = P.iend, oend = P.oend;
+    int32_t ip = P.ip, op = P.op;
+    InWindow& win = P.win;
+
+    // Fast path: a run of tokens with no length-extension bytes, far from
+    // both block ends, where the reference takes its two-stage shortcut
+    // (:150-191).  The token chain inside the 256-byte window at ip is found
+    // by pointer doubling: jump tables J_{2^i} (window offset -> offset 2^i
+    // tokens on, 255 = chain end; one byte per position, lane l holding
+    // positions 4l..4l+3) are composed with ds_bpermute gathers, then lane k
+    // follows the bits of k to token k.  Every field and check is then
+    // evaluated per lane.
+    if (ip <= iend - 18 && op <= oend - 32) {
+        win.follow(ip);
+        const int32_t r0 = ip - win.base;                  // < 256
+        const int32_t rin = iend - 18 - win.base;          // last token offset on the fast path
+        const int32_t jlim = (rin < 494 ? rin : 494) - r0;  // (offset bytes stay in A+B)
+        const uint32_t wv = win.rd4(ip + 4 * (int32_t)lane);
+        uint32_t J[6];
+        {
+            uint32_t j1 = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                const uint32_t t = (wv >> (8 * q)) & 0xFFu, p = 4 * lane + q;
+                const uint32_t n = p + (t >> 4) + 3;
+                const bool go = (t >> 4) != 15 && (t & 15) != 15 && (int32_t)p <= jlim && n <= 254;
+                j1 |= (go ? n : 255u) << (8 * q);
+            }
+            J[0] = j1;
+        }
+#pragma unroll
+        for (int i = 1; i < 6; ++i) J[i] = table_compose(J[i - 1], J[i - 1]);
+        uint32_t x = 0;  // lane k: window offset of token k (255: past the chain)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            const uint32_t y = table_at(J[i], x);
+            x = (lane >> i) & 1 ? y : x;
+        }
+        const uint32_t t = table_at(wv, x);  // token byte
+        const int32_t L = (int32_t)(t >> 4), Mt = (int32_t)(t & 15);
+        const bool cand = x != 255 && L != 15 && Mt != 15 && (int32_t)x <= jlim;
+        const int32_t lp = ip + (int32_t)x + 1;  // literal start
+        const int32_t off = cand ? (int32_t)win.rd16(lp + L) : 0;
+        const int32_t size = cand ? L + Mt + 4 : 0;
+        const int32_t incl = (int32_t)wave_incl_add((uint32_t)size);
+        const int32_t o_k = op + incl - size;
+        const int32_t m_k = o_k + L;
+        // the reference's checks on this path: shortcut entry (op <= oend-32,
+        // input side guaranteed by jlim), match inside the block (:299-302),
+        // and for offsets < 8 the _copy_match end check (:422-431)
+        const bool ok = cand && o_k <= oend - 32 && m_k >= off &&
+                        (off >= 8 || m_k + Mt + 4 <= oend - 5) && incl <= cap_out;
+        const uint64_t okm = ballot(ok);
+        const uint32_t nf = (~okm) ? ctz64(~okm) : kWave;  // first failing lane
+        if (nf > 0) {
+            b.ls = lp;
+            b.L = L;
+            b.op = o_k;
+            b.off = off;
+            b.M = Mt + 4;
+            b.n = nf;
+            P.op = op + lane_val((uint32_t)incl, nf - 1);
+            P.ip = lane_val((uint32_t)(lp + L + 2), nf - 1);  // the token after the last one
+            return kParsedFast;
+        }
+    }
+
+    // Exact scalar path (extension bytes, block ends, anything the fast path
+    // declined): one sequence.
+    win.follow(ip);  // ip now in window A: bytes up to ip + 256 are readable unchecked
+    const uint32_t r0 = (uint32_t)(ip - win.base);
+    const uint32_t token = win.ubyte(r0);
+    ip++;
+    uint32_t length = token >> 4;  // saturates at kSat
+    int32_t offset = 0, lit_ip, lit_op;
+    uint32_t L;
+
+    if (length != 15 && ip < P.shortiend && op <= P.shortoend) {
+        // Two-stage shortcut (:150-191): literals 0..14 fit, offset read.
+        lit_ip = ip;
+        lit_op = op;
+        L = length;
+        offset = (int32_t)win.ule16(r0 + 1 + length);
+        op += (int32_t)length;
+        ip += (int32_t)length + 2;
+        length = token & 15;
+        if (length != 15 && offset >= 8 && op >= offset) {
+            // 18-byte shortcut copy: match length 4..18, no checks left
+            length += 4;
+            goto record;
+        }
+        goto copy_match_checks;
+    }
+    if (length == 15) {  // :194-220
+        if (ip >= iend - 15) goto fail;
+        uint32_t s;
+        do {
+            s = win.byte(ip);
+            ip++;
+            length = length + s > kSat ? kSat : length + s;
+        } while (ip < iend - 15 && s == 255);
+    }
+    {
+        const uint32_t cpy = (uint32_t)op + length;  // :223-288
+        const uint32_t iln = (uint32_t)ip + length;
+        lit_ip = ip;
+        lit_op = op;
+        L = length;
+        if (ugt(cpy, oend - 12) || ugt(iln, iend - 8)) {
+            if (iln != (uint32_t)iend || ugt(cpy, oend)) goto fail;
+            ip += (int32_t)length;
+            op += (int32_t)length;
+            length = 0;
+            P.done = true;  // final literal run: no match
+            goto record;
+        }
+        ip += (int32_t)length;
+        op = (int32_t)cpy;
+    }
+    offset = (int32_t)(win.byte(ip) | (win.byte(ip + 1) << 8));  // :291-296
+    ip += 2;
+    length = token & 15;
+
+copy_match_checks:
+    // _copy_match (:298-336, :422-431)
+    if (op - offset < 0) goto fail;
+    if (length == 15) {
+        uint32_t s;
+        do {
+            s = win.byte(ip);
+            ip++;
+            if (ip > iend - 5) goto fail;
+            length = length + s > kSat ? kSat : length + s;
+        } while (s == 255);
+    }
+    if (ugt((uint32_t)op + length + 4, oend - 5)) goto fail;
+    length += 4;
+
+record:
+    {
+        const bool me = lane == 0;
+        b.ls = me ? lit_ip : 0;
+        b.L = me ? (int32_t)L : 0;
+        b.op = me ? lit_op : 0;
+        b.off = me ? offset : 0;
+        b.M = me ? (int32_t)length : 0;
+        b.n = 1;
+    }
+    P.op = op + (int32_t)length;
+    P.ip = ip;
+    return kParsedScalar;
+fail:
+    P.ip = ip;
+    return kParseFail;
+}
+
+// ---------------------------------------------------------------- batch copies
+
+// Copies of a scalar-path batch (one sequence, any length) in HBM: the
+// literal run, then the match; same-wave stores and loads to one global
+// address are ordered by the hardware (one vector L1 per CU) and the
+// wavefront fences keep the compiler from moving loads above the stores.
+LZ4E_DEV void copy_scalar_hbm(const Batch& b, const uint8_t* in, int32_t srcSize, uint8_t* gout,
+                              int32_t outSize, uint32_t lane) {
+    const int32_t L = lane_val((uint32_t)b.L, 0), op = lane_val((uint32_t)b.op, 0);
+    const int32_t ls = lane_val((uint32_t)b.ls, 0);
+    const int32_t M = lane_val((uint32_t)b.M, 0), off = lane_val((uint32_t)b.off, 0);
+    wave_fence();
+    if (L > 0 && L <= kLong) {
+        if (lane == 0) lane_copy64(gout + op, in + ls, L, in + srcSize);
+    } else if (L > kLong) {
+        wave_copy(gout + op, in + ls, L, lane);
+    }
+    wave_fence();
+    const int32_t ms = op + L;
+    if (M > 0 && M <= kLong) {
+        if (lane == 0) lane_match(gout + ms, (uint32_t)off, M, gout + outSize);
+    } else if (M > kLong) {
+        wave_match(gout, ms, (uint32_t)off, M, lane);
+    }
+    wave_fence();
+}
+
 struct Stamps {
     uint64_t t = 0, acc[4] = {0, 0, 0, 0}, batches = 0, rounds = 0;
 };
 
-// Decode one block into HBM.  LDS: the input ring, the store sink and the
-// span buffer of the fast batches.
+// Decode one block into HBM on one wave.  LDS: the input ring, the store
+// sink, the span buffer of the fast batches and its jump table.
 template <bool kStamps>
 LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, int32_t outSize,
                            int32_t* ret_slot, uint64_t* dbg, uint32_t lane, lu8* span,
@@ -490,210 +717,49 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
     };
     if constexpr (kStamps) st.t = clock64();
     lu8* sink = (lu8*)ring + kRing + kRingPad + 4 * lane;  // (span follows the sink)
+    Parse P;
+    P.init(in, srcSize, outSize, ring, lane);
 
-    InWindow win;
-    {
-        const uintptr_t a = reinterpret_cast<uintptr_t>(in);
-        win.shift = (int32_t)(a & 3);
-        win.w = (gcu32*)(a - win.shift);
-        win.last = (srcSize + win.shift - 1) >> 2;
-        win.lane = lane;
-        win.ring = ring;
-        win.reload(0);
-    }
-
-    const int32_t iend = srcSize, oend = outSize;
-    const int32_t shortiend = iend - 14 - 2;  // :100-101
-    const int32_t shortoend = oend - 14 - 18; // :102-103
-    int32_t ip = 0, op = 0;
-    bool done = false;
-
-    while (!done) {
-        // ------------------------------------------------ 1. parse a batch
-        int32_t r_ls = 0, r_L = 0, r_op = 0, r_off = 0, r_M = 0;  // lane k: sequence k
-        uint32_t nseq = 0;
-        bool fastb = false;  // the batch came from the fast path (span-staged copies)
-
-        // 1a. Fast path: a run of tokens with no length-extension bytes, far
-        // from both block ends, where the reference takes its two-stage
-        // shortcut (:150-191).  The token chain inside the 256-byte window at
-        // ip is found by pointer doubling: jump tables J_{2^i} (window offset
-        // -> offset 2^i tokens on, 255 = chain end; one byte per position,
-        // lane l holding positions 4l..4l+3) are composed with ds_bpermute
-        // gathers, then lane k follows the bits of k to token k.  Every field
-        // and check is then evaluated per lane.
-        if (ip <= iend - 18 && op <= oend - 32) {
-            win.follow(ip);
-            const int32_t r0 = ip - win.base;                  // < 256
-            const int32_t rin = iend - 18 - win.base;          // last token offset on the fast path
-            const int32_t jlim = (rin < 494 ? rin : 494) - r0;  // (offset bytes stay in A+B)
-            const uint32_t wv = win.rd4(ip + 4 * (int32_t)lane);
-            uint32_t J[6];
-            {
-                uint32_t j1 = 0;
-#pragma unroll
-                for (uint32_t q = 0; q < 4; ++q) {
-                    const uint32_t t = (wv >> (8 * q)) & 0xFFu, p = 4 * lane + q;
-                    const uint32_t n = p + (t >> 4) + 3;
-                    const bool go = (t >> 4) != 15 && (t & 15) != 15 && (int32_t)p <= jlim && n <= 254;
-                    j1 |= (go ? n : 255u) << (8 * q);
-                }
-                J[0] = j1;
-            }
-#pragma unroll
-            for (int i = 1; i < 6; ++i) J[i] = table_compose(J[i - 1], J[i - 1]);
-            uint32_t x = 0;  // lane k: window offset of token k (255: past the chain)
-#pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const uint32_t y = table_at(J[i], x);
-                x = (lane >> i) & 1 ? y : x;
-            }
-            const uint32_t t = table_at(wv, x);  // token byte
-            const int32_t L = (int32_t)(t >> 4), Mt = (int32_t)(t & 15);
-            const bool cand = x != 255 && L != 15 && Mt != 15 && (int32_t)x <= jlim;
-            const int32_t lp = ip + (int32_t)x + 1;  // literal start
-            const int32_t off = cand ? (int32_t)win.rd16(lp + L) : 0;
-            const int32_t size = cand ? L + Mt + 4 : 0;
-            const int32_t incl = (int32_t)wave_incl_add((uint32_t)size);
-            const int32_t o_k = op + incl - size;
-            const int32_t m_k = o_k + L;
-            // the reference's checks on this path: shortcut entry (op <= oend-32,
-            // input side guaranteed by jlim), match inside the block (:299-302),
-            // and for offsets < 8 the _copy_match end check (:422-431)
-            const bool ok = cand && o_k <= oend - 32 && m_k >= off &&
-                            (off >= 8 || m_k + Mt + 4 <= oend - 5);
-            const uint64_t okm = ballot(ok);
-            const uint32_t nf = (~okm) ? ctz64(~okm) : kWave;  // first failing lane
-            if (nf > 0) {
-                fastb = true;
-                r_ls = lp;
-                r_L = L;
-                r_op = o_k;
-                r_off = off;
-                r_M = Mt + 4;
-                nseq = nf;
-                op += lane_val((uint32_t)incl, nf - 1);
-                ip = lane_val((uint32_t)(lp + L + 2), nf - 1);  // the token after the last one
-            }
-        }
-
-        // 1b. Exact scalar path (extension bytes, block ends, anything the
-        // fast path declined): until the fast path applies again.
-        while (nseq == 0) {
-            win.follow(ip);  // ip now in window A: bytes up to ip + 256 are readable unchecked
-            const uint32_t r0 = (uint32_t)(ip - win.base);
-            const uint32_t token = win.ubyte(r0);
-            ip++;
-            uint32_t length = token >> 4;  // saturates at kSat
-            int32_t offset = 0, lit_ip, lit_op;
-            uint32_t L;
-
-            if (length != 15 && ip < shortiend && op <= shortoend) {
-                // Two-stage shortcut (:150-191): literals 0..14 fit, offset read.
-                lit_ip = ip;
-                lit_op = op;
-                L = length;
-                offset = (int32_t)win.ule16(r0 + 1 + length);
-                op += (int32_t)length;
-                ip += (int32_t)length + 2;
-                length = token & 15;
-                if (length != 15 && offset >= 8 && op >= offset) {
-                    // 18-byte shortcut copy: match length 4..18, no checks left
-                    length += 4;
-                    goto record;
-                }
-                goto copy_match_checks;
-            }
-            if (length == 15) {  // :194-220
-                if (ip >= iend - 15) goto fail;
-                uint32_t s;
-                do {
-                    s = win.byte(ip);
-                    ip++;
-                    length = length + s > kSat ? kSat : length + s;
-                } while (ip < iend - 15 && s == 255);
-            }
-            {
-                const uint32_t cpy = (uint32_t)op + length;  // :223-288
-                const uint32_t iln = (uint32_t)ip + length;
-                lit_ip = ip;
-                lit_op = op;
-                L = length;
-                if (ugt(cpy, oend - 12) || ugt(iln, iend - 8)) {
-                    if (iln != (uint32_t)iend || ugt(cpy, oend)) goto fail;
-                    ip += (int32_t)length;
-                    op += (int32_t)length;
-                    length = 0;
-                    done = true;  // final literal run: no match
-                    goto record;
-                }
-                ip += (int32_t)length;
-                op = (int32_t)cpy;
-            }
-            offset = (int32_t)(win.byte(ip) | (win.byte(ip + 1) << 8));  // :291-296
-            ip += 2;
-            length = token & 15;
-
-        copy_match_checks:
-            // _copy_match (:298-336, :422-431)
-            if (op - offset < 0) goto fail;
-            if (length == 15) {
-                uint32_t s;
-                do {
-                    s = win.byte(ip);
-                    ip++;
-                    if (ip > iend - 5) goto fail;
-                    length = length + s > kSat ? kSat : length + s;
-                } while (s == 255);
-            }
-            if (ugt((uint32_t)op + length + 4, oend - 5)) goto fail;
-            length += 4;
-
-        record:
-            {
-                const bool me = lane == nseq;  // v_cndmask into lane nseq
-                r_ls = me ? lit_ip : r_ls;
-                r_L = me ? (int32_t)L : r_L;
-                r_op = me ? lit_op : r_op;
-                r_off = me ? offset : r_off;
-                r_M = me ? (int32_t)length : r_M;
-            }
-            op += (int32_t)length;
-            nseq++;
+    for (;;) {
+        Batch b;
+        const ParseResult pr = parse_batch(P, b, lane);
+        if (pr == kParseFail) {
+            if (lane == 0) *ret_slot = -P.ip - 1;
             break;
         }
         lap(0);
         if constexpr (kStamps) st.batches++;
-        const bool valid = lane < nseq;
-        if (fastb) {
+        const bool valid = lane < b.n;
+        const int32_t op = P.op;  // end of the batch's output
+        if (pr == kParsedFast) {
             // ---------------- span-staged copies (fast batches) -------------
             // The batch's output [lo, op) (<= 64 x 32 bytes) is assembled in
             // LDS: literals from the ring; the part of a match source that
             // lies before lo from HBM (final: written by earlier batches);
             // the rest in LDS dependency rounds.  Then one store pass.
-            const int32_t lo = lane_val((uint32_t)r_op, 0);
+            const int32_t lo = lane_val((uint32_t)b.op, 0);
             const int32_t a0 = lo & ~15;  // span index of position x: x - a0
-            const int32_t ms = r_op + r_L, ss = ms - r_off;
+            const int32_t ms = b.op + b.L, ss = ms - b.off;
             int32_t n0 = 0;
             uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0;
             if (valid && ss < lo) {  // fast path: lo <= oend - 32, so [ss, ss + 32) is in the block
-                n0 = r_M < lo - ss ? r_M : lo - ss;
+                n0 = b.M < lo - ss ? b.M : lo - ss;
                 h0 = ldg16(gout + ss);
                 if (n0 > 16) h1 = ldg16(gout + ss + 16);
             }
-            if (valid && r_L > 0) {
-                const lu8* rs = win.in_ring(r_ls, r_L);
-                if (rs) lane_copy(span + (r_op - a0), rs, r_L, sink);
-                else lane_copy64(span + (r_op - a0), in + r_ls, r_L, in + srcSize);
+            if (valid && b.L > 0) {
+                const lu8* rs = P.win.in_ring(b.ls, b.L);
+                if (rs) lane_copy(span + (b.op - a0), rs, b.L, sink);
+                else lane_copy64(span + (b.op - a0), in + b.ls, b.L, in + srcSize);
             }
             if (n0 > 0) {
                 put16(span + (ms - a0), h0, n0 < 16 ? n0 : 16, sink);
                 if (n0 > 16) put16(span + (ms - a0) + 16, h1, n0 - 16, sink);
             }
             lap(1);
-            const int32_t ms2 = ms + n0, m2 = r_M - n0, me = ms + r_M;
+            const int32_t ms2 = ms + n0, m2 = b.M - n0, me = ms + b.M;
             const int32_t ss2 = ss + n0;
-            const int32_t need = me - r_off < ms2 ? me - r_off : ms2;  // source part before own output
+            const int32_t need = me - b.off < ms2 ? me - b.off : ms2;  // source part before own output
             uint64_t pending = ballot(valid && m2 > 0);
             while (pending) {
                 // ready when [ss2, need) overlaps no earlier pending output
@@ -708,13 +774,12 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
                     // ready): resolve every pending byte by pointer jumping.
                     const int32_t s0 = (int32_t)lane_val((uint32_t)ms2, ctz64(pending)) - a0;
                     const uint32_t nr = resolve_chains(span, jump, lo - a0, op - a0, s0, mine,
-                                                       ms2 - a0, m2, r_off, lane);
+                                                       ms2 - a0, m2, b.off, lane);
                     if constexpr (kStamps) st.rounds += nr;
-                    pending = 0;
                     break;
                 }
                 if (ready) {
-                    if (r_off != 0) lane_match(span + (ms2 - a0), (uint32_t)r_off, m2, sink);
+                    if (b.off != 0) lane_match(span + (ms2 - a0), (uint32_t)b.off, m2, sink);
                     else lane_zero(span + (ms2 - a0), m2, sink);
                 }
                 pending &= ~rm;
@@ -734,64 +799,16 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
                 }
             }
             lap(3);
-            continue;
+        } else {
+            // ---------------- in-HBM copies (scalar-path batches) -----------
+            copy_scalar_hbm(b, in, srcSize, gout, outSize, lane);
+            lap(2);
         }
-        // ---------------- in-HBM copies (scalar-path batches) ---------------
-        // ------------------------------------------------ 2. literals
-        wave_fence();
-        if (valid && r_L > 0 && r_L <= kLong) lane_copy64(gout + r_op, in + r_ls, r_L, in + srcSize);
-        {
-            uint64_t longs = ballot(valid && r_L > kLong);
-            while (longs) {
-                const uint32_t j = ctz64(longs);
-                longs &= longs - 1;
-                wave_copy(gout + lane_val(r_op, j), in + lane_val(r_ls, j), (int32_t)lane_val(r_L, j),
-                          lane);
-            }
+        if (P.done) {
+            if (lane == 0) *ret_slot = P.op;
+            break;
         }
-        wave_fence();
-        lap(1);
-
-        // ------------------------------------------------ 3. matches
-        {
-            const int32_t ms = r_op + r_L;  // match start
-            const int32_t me = ms + r_M;    // match end
-            const int32_t need = me - r_off < ms ? me - r_off : ms;  // source part before own output
-            const int32_t ss = ms - r_off;  // source start
-            const int32_t batch_lo = lane_val(r_op, 0);
-            uint64_t pending = ballot(valid && r_M > 0);
-            while (pending) {
-                // Ready when [ss, need) is final: before this batch's output, or
-                // before every pending earlier match, or after all of them.
-                const bool mine = (pending >> lane) & 1;
-                const bool quick = need <= batch_lo;
-                bool ready = mine && quick;
-                if (ballot(mine && !quick)) {
-                    const int32_t mn = wave_excl_min(mine ? ms : INT32_MAX);
-                    const int32_t mx = wave_excl_max(mine ? me : INT32_MIN);
-                    ready = mine && (quick || need <= mn || ss >= mx);
-                }
-                if (ready && r_M <= kLong) lane_match(gout + ms, (uint32_t)r_off, r_M, gout + outSize);
-                wave_fence();
-                uint64_t longs = ballot(ready && r_M > kLong);
-                while (longs) {
-                    const uint32_t j = ctz64(longs);
-                    longs &= longs - 1;
-                    wave_match(gout, lane_val(ms, j), lane_val(r_off, j), lane_val(r_M, j), lane);
-                    wave_fence();
-                }
-                pending &= ~ballot(ready);
-                if constexpr (kStamps) st.rounds++;
-            }
-        }
-        wave_fence();
-        lap(2);
     }
-    if (lane == 0) *ret_slot = op;
-    goto finish;
-fail:
-    if (lane == 0) *ret_slot = -ip - 1;
-finish:
     if constexpr (kStamps) {
         if (lane == 0 && dbg) {
             dbg[0] = st.acc[0];
@@ -841,7 +858,7 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
     uint8_t* out = dst + dst_off[b];
     uint64_t* d = kStamps && dbg ? dbg + 8 * (size_t)b : nullptr;
     if (special_case(in, srcSize, outSize, ret + b, lane)) return;
-    // LDS: [input ring + mirror] [store sink] [span]
+    // LDS: [input ring + mirror] [store sink] [span] [jump table]
     __shared__ __attribute__((aligned(16))) uint8_t smem[kRing + kRingPad + kSink + kSpan + kJump];
     decode_block<kStamps>(in, srcSize, out, outSize, ret + b, d, lane,
                           (lu8*)(smem + kRing + kRingPad + kSink), (lu32*)smem,
@@ -849,543 +866,435 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
 }
 
 // ============================================================================
-// Workgroup decoder: one block per 256-thread workgroup, output image in LDS
+// Pipelined decoder: one block per 4-wave workgroup
 // ============================================================================
 //
-// For blocks whose capacity is at most 64 KiB (the 4 KiB and 64 KiB chunk
-// sizes).  The one-wave decoder above is bound by its serial chain: one
-// batch of <= 64 sequences at a time, and dependent short matches (records,
-// integer tables) resolved a few bytes per lane per round.  Here the four
-// waves of a workgroup share the block:
+// The one-wave decoder above runs the parse and the copies of each batch one
+// after the other, and a block's time is the sum of both over its ~150
+// batches; with ~3 blocks per SIMD the kernel time is the slowest block's
+// chain.  Here the parse and the copies of different batches overlap:
 //
-//  1. Parse, a 1 KiB window of the token stream per batch.  Every window
-//     position is parsed speculatively as if a token started there (its next
-//     token position J1, extension bytes included); the true tokens are the
-//     orbit of the window's first position, found by pointer doubling over
-//     J (J2 = J1 o J1, ...) with the marking rule
-//     mark(J_{2^k}(p)) |= mark(p): after 9 levels every chain element of
-//     index < 512 (> the 342 tokens a 1 KiB window can hold) is marked.
-//     A workgroup scan over the marks gives each token its rank and output
-//     position.
-//  2. Check, per token, every bound the reference tests on its path
-//     (lz4e_decompress.c:123-446: the two-stage shortcut's entry
-//     conditions, literal end margins, extension-byte limits, offset inside
-//     the output, match end margin, the exact final literal run).  A block
-//     with any token that fails them -- malformed input, a too-small
-//     capacity -- is decoded from scratch by the one-wave exact decoder
-//     above (wave 0), so return values and error codes are the reference's
-//     by construction.  Blocks that pass produce the reference's bytes: its
-//     copies implement plain LZ semantics (offset 0 writes zeros).
-//  3. Literals: per sequence, long runs by the whole workgroup.
-//  4. Matches, in output sub-spans of 2 KiB: every byte finds its sequence
-//     (scatter of sequence starts + max scan), a byte whose source lies
-//     before the sub-span (self-overlap folded: out[m + t] =
-//     out[m - off + t mod off]) or in a literal is final at once; the rest
-//     point at their source byte and resolve by pointer jumping (a chain of
-//     depth d in log2 d rounds).
-//  5. The finished image leaves LDS in 16-byte stores.
-constexpr uint32_t kWgT = 256;                  // threads per workgroup (4 waves)
-constexpr uint32_t kWgWaves = kWgT / kWave;
-constexpr uint32_t kWin = 1024;                 // token-stream bytes parsed per batch
-constexpr uint32_t kWinPad = 256;               // staged bytes past the window
-constexpr uint32_t kMaxSeq = kWin / 3 + 2;      // a non-final sequence takes >= 3 input bytes
-constexpr uint32_t kSub = 2048;                 // output bytes resolved per sub-span
-constexpr uint32_t kOutMax = 65536;             // largest capacity this decoder takes
-constexpr uint32_t kLevels = 9;                 // 2^9 > kMaxSeq
-constexpr uint16_t kNone = 0xFFFF;              // no target / final byte
-constexpr uint32_t kLongLit = 64;               // longer literal runs: whole workgroup
-constexpr uint32_t kMaxLong = 32;
-constexpr uint32_t kLenCap = 1u << 20;          // speculative lengths saturate here
+//  * wave 0 parses (parse_batch: the reference's exact checks, so the return
+//    value is decided here) and publishes each batch -- per-lane sequence
+//    records plus its output range [lo, hi) -- in a ring of record slots;
+//  * waves 1..3 (copier c = wave - 1) copy batches j = c, c+3, c+6, ... so
+//    three batches are in flight at once.  A fast batch (at most kPipeOut
+//    output bytes) is assembled in an LDS span; every output byte is a
+//    literal (from the compressed input in HBM), a match byte whose source
+//    lies before the far line F (final in HBM: loaded), one whose source lies
+//    in the batch itself (internal pointer) or one whose source lies in the
+//    spans of batches j-1 / j-2, still in LDS (cross pointer).  Match byte t
+//    of a sequence copies output byte x - off, also inside a self-overlapping
+//    match, so the pointers are linear in t.  Internal pointers resolve by
+//    pointer jumping (a chain of depth d in log2 d rounds) in parallel with
+//    the other copiers; only the gather of the cross bytes waits for batches
+//    j-1 and j-2, and that is one LDS round trip, so the batches' serial
+//    chain is short.  The span then leaves in 16-byte stores.  A scalar-path
+//    batch (long runs, block ends) copies in HBM once every earlier batch is
+//    stored.
+//
+// Progress flags (LDS, workgroup-scope acquire/release): `resolved` counts
+// the batches whose bytes are final (in order), `stored` is the output
+// prefix known to be in HBM (each batch's stores waited for with
+// s_waitcnt vmcnt(0) before it moves, in order).  Far loads wait for
+// stored >= F.  Measured against per-copier flags (batches finishing out of
+// order, "all batches <= k" read off three flags): the in-order counters
+// poll one word instead of three and were 10 % faster on silesia64k.  Every
+// wait is bounded (watchdog).
+constexpr uint32_t kPipeWaves = 4;
+constexpr uint32_t kCopiers = kPipeWaves - 1;
+constexpr uint32_t kPipeRecs = 4;
+constexpr uint32_t kPipeSpans = 5;
+constexpr int32_t kPipeOut = 1024;                   // output bytes per fast batch
+constexpr uint32_t kPipeSpan = kPipeOut + 16 + 48;   // its span (16-B aligned start)
+constexpr uint16_t kCross = 0x8000;  // jump entry: 0x8000 | (source - F)
+enum : int32_t { kKindFast = 0, kKindHbm = 1 };
+// record header: sequences, kind, output range, far line F, the starts of
+// batches j-1 and j-2
+enum { kHdrN, kHdrKind, kHdrLo, kHdrHi, kHdrF, kHdrLo1, kHdrLo2, kHdrWords = 8 };
 
-struct WgLds {
-    uint8_t out[kOutMax + 16];
-    uint8_t win[kWin + kWinPad + 16];
-    union {
-        struct {
-            uint16_t a[kWin], b[kWin];  // J_{2^k}, J_{2^{k+1}} (window offsets)
-        } j;
-        uint16_t ptr[kSub];  // sub-span: sequence id + 1, then source byte / kNone
-    } u;
-    uint8_t mark[kWin];
-    uint32_t s_op[kMaxSeq], s_lit[kMaxSeq], s_len[kMaxSeq], s_off[kMaxSeq], s_m4[kMaxSeq];
-    uint32_t red[4 * kWgWaves];
-    uint32_t longs[kMaxLong];
-    int32_t st[8];
-};
-static_assert(sizeof(WgLds) <= 81920, "two workgroups per CU");
-static_assert(kRing + kRingPad + kSink + kSpan + kJump <= kOutMax, "fallback LDS inside the image");
-
-typedef __attribute__((address_space(1))) const uint8_t gcu8;
-typedef __attribute__((address_space(1))) const u32a1 gcu32a1;
-
-// The staged window [ip0, ip0 + kWin + kWinPad) from LDS, anything else from
-// HBM (zero past the input, like the staging).
-struct WinSrc {
-    const uint8_t* win;
-    gcu8* in;
-    int32_t n, ip0;
-    LZ4E_DEV uint32_t at(int32_t q) const {
-        const uint32_t r = (uint32_t)(q - ip0);
-        if (r < kWin + kWinPad) return win[r];
-        return q < n ? in[q] : 0u;
-    }
+struct PipeLds {
+    uint32_t ring[(kRing + kRingPad) / 4];     // parser input ring
+    int32_t rec[kPipeRecs][5][kWave];          // ls, L, op, off, M per sequence
+    int32_t hdr[kPipeRecs][kHdrWords];
+    uint8_t span[kPipeSpans][kPipeSpan];
+    uint16_t jump[kCopiers][kPipeSpan];
+    uint8_t sink[kCopiers][kSink];
+    int32_t pub[kPipeRecs], con[kPipeRecs];    // record slot published / consumed (batch index)
+    int32_t resolved;                          // batches whose bytes are final, in order
+    int32_t stored;                            // output prefix known to be in HBM
+    int32_t nb_total;                          // batches, once the parser is done
+    int32_t abort;                             // a wait timed out (watchdog): every wave leaves
 };
 
-// One sequence read as if a token started at t (lz4e_decompress.c:123-336
-// field layout): literal start/length, offset, position after the match
-// length's extension bytes (the next token), match length + MINMATCH.
-struct Tok {
-    uint32_t token, lit, len, off, xm, m4;
-};
+// Watchdog of the waits: a wait that outlasts ~2^23 sleeps (~1 s) means a
+// broken invariant; the block then fails (ret = kPipeAbort) instead of hanging.
+constexpr uint32_t kSpinMax = 1u << 23;
+constexpr int32_t kPipeAbort = INT32_MIN;
 
-LZ4E_DEV Tok parse_tok(const WinSrc& S, int32_t t) {
-    Tok k;
-    k.token = S.at(t);
-    uint32_t L = k.token >> 4, M = k.token & 15;
-    int32_t x = t + 1;
-    if (L == 15) {
-        uint32_t s;
-        do {
-            s = S.at(x++);
-            L += s;
-        } while (s == 255 && x < S.n && L < kLenCap);
-    }
-    k.lit = (uint32_t)x;
-    k.len = L;
-    x += (int32_t)L;
-    k.off = S.at(x) | (S.at(x + 1) << 8);
-    x += 2;
-    if (M == 15) {
-        uint32_t s;
-        do {
-            s = S.at(x++);
-            M += s;
-        } while (s == 255 && x < S.n && M < kLenCap);
-    }
-    k.xm = (uint32_t)x;
-    k.m4 = M + 4;
-    return k;
+LZ4E_DEV int32_t lds_acquire(int32_t* p) {
+    return (int32_t)uni((uint32_t)__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+LZ4E_DEV void lds_release(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// Every global store of this wave has completed (before a flag says so).
+LZ4E_DEV void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// u16 x 4 at a jump-table index (unaligned forms for the pointer runs).
+typedef uint64_t __attribute__((aligned(2))) u64a2;
+typedef __attribute__((address_space(3))) u64a2 lu64a2;
+typedef __attribute__((address_space(3))) uint64_t lu64;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lu128;
+LZ4E_DEV int32_t wave_min_i32(int32_t v) {
+    const int32_t e = wave_excl_min(v);
+    const int32_t m = e < v ? e : v;
+    return (int32_t)lane_val((uint32_t)m, kWave - 1);
 }
 
-// Next-token offset of window position r if a token started there, or kNone
-// when that lies at or past the window end (only the staged bytes are read:
-// anything longer leaves the window anyway).
-LZ4E_DEV uint16_t jump1(const uint8_t* win, uint32_t r) {
-    const uint32_t tok = win[r];
-    uint32_t L = tok >> 4, x = r + 1;
-    if (L == 15) {
-        uint32_t s;
-        do {
-            s = win[x++];
-            L += s;
-        } while (s == 255 && x < kWin);
-    }
-    x += L + 2;
-    if (x >= kWin) return kNone;
-    if ((tok & 15) == 15) {
-        uint32_t s;
-        do {
-            s = win[x++];
-        } while (s == 255 && x < kWin);
-    }
-    return x < kWin ? (uint16_t)x : kNone;
-}
 
-// Exclusive workgroup prefix sums of two values; totals through t0 / t1.
-LZ4E_DEV void wg_scan2(uint32_t v0, uint32_t v1, uint32_t* red, uint32_t tid, uint32_t& e0,
-                       uint32_t& e1, uint32_t& t0, uint32_t& t1) {
-    const uint32_t i0 = wave_incl_add(v0), i1 = wave_incl_add(v1);
-    const uint32_t w = tid / kWave;
-    if (tid % kWave == kWave - 1) {
-        red[w] = i0;
-        red[kWgWaves + w] = i1;
-    }
-    __syncthreads();
-    uint32_t b0 = 0, b1 = 0, s0 = 0, s1 = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kWgWaves; ++i) {
-        const uint32_t r0 = red[i], r1 = red[kWgWaves + i];
-        if (i < w) b0 += r0, b1 += r1;
-        s0 += r0, s1 += r1;
-    }
-    __syncthreads();
-    e0 = b0 + i0 - v0;
-    e1 = b1 + i1 - v1;
-    t0 = s0;
-    t1 = s1;
-}
-
-// Exclusive workgroup prefix max of values >= 0 (0 for the first thread).
-LZ4E_DEV int32_t wg_excl_max(int32_t v, uint32_t* red, uint32_t tid) {
-    const int32_t ex = wave_excl_max(v);  // lane 0: INT32_MIN
-    const int32_t in = ex > v ? ex : v;
-    const uint32_t w = tid / kWave;
-    if (tid % kWave == kWave - 1) red[2 * kWgWaves + w] = (uint32_t)in;
-    __syncthreads();
-    int32_t b = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < kWgWaves; ++i)
-        if (i < w) b = b > (int32_t)red[2 * kWgWaves + i] ? b : (int32_t)red[2 * kWgWaves + i];
-    __syncthreads();
-    return b > ex ? b : ex;
-}
-
-// len literal bytes at lit into the image at o (one thread).
-LZ4E_DEV void lit_copy(uint8_t* out, uint32_t o, const WinSrc& S, uint32_t lit, uint32_t len) {
-    const uint32_t r = lit - (uint32_t)S.ip0;
-    uint8_t* d = out + o;
-    uint32_t k = 0;
-    if (r + len <= kWin + kWinPad) {
-        const uint8_t* s = S.win + r;
-        for (; k + 4 <= len; k += 4) st4((lu8*)(d + k), ld4((const lu8*)(s + k)));
-        for (; k < len; ++k) d[k] = s[k];
-    } else {
-        gcu8* s = S.in + lit;
-        for (; k + 4 <= len; k += 4) st4((lu8*)(d + k), *(gcu32a1*)(s + k));
-        for (; k < len; ++k) d[k] = s[k];
-    }
-}
-
-// The one-wave exact decoder on wave 0 (reference bound checks and error
-// codes), LDS carved from the image.
-LZ4E_DEV void wg_fallback(WgLds& L, const uint8_t* in, int32_t srcSize, uint8_t* gout,
-                          int32_t outSize, int32_t* ret_slot, uint32_t tid) {
-    if (tid >= kWave) return;
-    uint8_t* smem = L.out;
-    decode_block<false>(in, srcSize, gout, outSize, ret_slot, nullptr, tid,
-                        (lu8*)(smem + kRing + kRingPad + kSink), (lu32*)smem,
-                        (lu16*)(smem + kRing + kRingPad + kSink + kSpan));
-}
-
-// Phase cycle counters of the diagnostic build (tid 0's clock; phases are
-// separated by workgroup barriers): stage+J1, doubling, tokens, literals,
-// matches, flush, batches, sub-span rounds.
-struct WgStamps {
-    uint64_t t = 0, acc[6] = {0, 0, 0, 0, 0, 0}, batches = 0, rounds = 0;
-    LZ4E_DEV void lap(bool on, int ph) {
+// Cycle counters of the stamped build, per block (u64 x 16): parser parse,
+// parser waits, copier other work, copier waits for records, for far loads,
+// for batch j-1 (resolved), for the in-order store flag, batches; copier
+// phases: loads + span setup, internal rounds, cross gather, store pass,
+// store completion; internal rounds, batches with internal pointers.
+enum { kStParse, kStPWait, kStWork, kStRec, kStFar, kStPrev, kStStore, kStBatches, kStLoads,
+       kStRounds, kStGather, kStSpass, kStVm, kStNRounds, kStNInt, kStUnused, kStSlots };
+struct PipeStamps {
+    uint64_t acc[kStSlots] = {};
+    uint64_t t = 0;
+    LZ4E_DEV void lap(bool on, int k) {
         if (!on) return;
         const uint64_t now = clock64();
-        acc[ph] += now - t;
+        acc[k] += now - t;
         t = now;
     }
 };
 
+// Waits until ready(); false when the watchdog fired (here or in another wave).
+template <class F>
+LZ4E_DEV bool wait_for(PipeLds& S, F ready) {
+    for (uint32_t k = 0; !ready(); ++k) {
+        if (k >= kSpinMax || lds_acquire(&S.abort)) {
+            lds_release(&S.abort, 1);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+}
+
+template <bool kStamps, class F>
+LZ4E_DEV bool spin(PipeLds& S, F ready, PipeStamps& st, int k) {
+    st.lap(kStamps, kStWork);
+    const bool ok = wait_for(S, ready);
+    st.lap(kStamps, k);
+    return ok;
+}
+
+// A fast batch j (see above).  Slot safety with 3 copiers in round robin:
+// span slot j % 5 last held batch j-5, read by batches j-4 and j-3 (cross
+// gathers) and by its own store pass; j-3 was this wave's previous batch,
+// j-4's gather happened before `resolved` reached j-3 (this wave waited for
+// that), and j-5 was stored before this wave's batch j-3 could be.
 template <bool kStamps>
-__global__ __launch_bounds__(kWgT) void decompress_wg_kernel(const uint8_t* __restrict__ src,
-                                                             const uint64_t* __restrict__ src_off,
-                                                             const int32_t* __restrict__ src_len,
-                                                             uint8_t* dst,
-                                                             const uint64_t* __restrict__ dst_off,
-                                                             const int32_t* __restrict__ dst_cap,
-                                                             int32_t* __restrict__ ret,
-                                                             uint32_t nblocks,
-                                                             uint64_t* __restrict__ dbg) {
-    __shared__ __attribute__((aligned(16))) WgLds L;
-    WgStamps stp;
-    const bool on = kStamps && threadIdx.x == 0;
-    if (on) stp.t = clock64();
+LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const int32_t* hdr,
+                        const uint8_t* in, int32_t srcSize, uint8_t* gout, uint32_t lane,
+                        PipeStamps& st) {
+    const int32_t lo = hdr[kHdrLo], hi = hdr[kHdrHi], F = hdr[kHdrF];
+    const int32_t a0 = lo & ~15;
+    const int32_t s0 = lo - a0, s1 = hi - a0;  // span indices of [lo, hi)
+    lu8* span = (lu8*)S.span[(uint32_t)j % kPipeSpans];
+    lu16* jt = (lu16*)S.jump[c];
+    lu8* sink = (lu8*)S.sink[c] + 4 * lane;
+    const bool valid = lane < b.n;
+    const int32_t ms = b.op + b.L, ss = ms - b.off;
+    // Match byte t of a sequence copies output byte ss + t; bytes [0, nf)
+    // come from before F (HBM).
+    int32_t nf = 0;
+    if (valid && b.off != 0 && ss < F) nf = b.M < F - ss ? b.M : F - ss;
+    if (ballot(nf > 0) &&
+        !spin<kStamps>(S, [&] { return lds_acquire(&S.stored) >= F; }, st, kStFar))
+        return false;
+    // loads first (far source bytes, the literal run), consumed below
+    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, lv = h0;
+    if (nf > 0) {
+        h0 = ldg16(gout + ss);
+        if (nf > 16) h1 = ldg16(gout + ss + 16);
+    }
+    const bool lfast = valid && b.L > 0 && b.ls + 16 <= srcSize;
+    if (lfast) lv = ldg16(in + b.ls);
+    // every byte of [lo, hi) final until shown otherwise
+#pragma unroll 4
+    for (int32_t i = s0 + (int32_t)lane; i < s1; i += kWave) jt[i] = kFinal;
+    wave_fence();
+    // match bytes [nf, M): a cross pointer below lo, else an internal one
+    const bool ptrs = valid && b.off != 0 && nf < b.M;
+    if (ptrs) {
+        lu16* e = jt + (ms - a0);
+        for (int32_t t = nf; t < b.M; ++t) {
+            const int32_t y = ss + t;
+            e[t] = (uint16_t)(y < lo ? (int32_t)kCross + (y - F) : y - a0);
+        }
+    }
+    const bool has_cross = ptrs && ss + nf < lo;
+    const bool has_int = ptrs && ss + b.M > lo;
+    // rounds and gather start at the first pointer byte
+    const int32_t i0 = (int32_t)uni((uint32_t)wave_min_i32(ptrs ? ms + nf - a0 : s1));
+    // the loaded bytes into the span
+    if (valid && b.L > 0) {
+        if (lfast) put16(span + (b.op - a0), lv, (uint32_t)b.L, sink);
+        else
+#pragma clang loop unroll(disable) vectorize(disable)
+            for (int32_t t = 0; t < b.L; ++t) span[b.op - a0 + t] = in[b.ls + t];
+    }
+    if (nf > 0) {
+        put16(span + (ms - a0), h0, nf < 16 ? nf : 16, sink);
+        if (nf > 16) put16(span + (ms - a0) + 16, h1, nf - 16, sink);
+    }
+    if (valid && b.off == 0)  // offset 0 writes zeros (:313, 407-415)
+#pragma clang loop unroll(disable) vectorize(disable)
+        for (int32_t t = 0; t < b.M; ++t) span[ms - a0 + t] = 0;
+    wave_fence();
+    st.lap(kStamps, kStLoads);
+    // internal pointers: pointer jumping until each byte is final or cross
+    // (four span bytes per lane per step: their reads are independent)
+    if (ballot(has_int)) {
+        if (kStamps) st.acc[kStNInt]++;
+        for (;;) {
+            if (kStamps) st.acc[kStNRounds]++;
+            bool more = false;
+            for (int32_t g = i0 + (int32_t)lane; g < s1; g += 4 * kWave) {
+                uint32_t v[4], w[4], sv[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int32_t i = g + q * (int32_t)kWave;
+                    v[q] = i < s1 ? jt[i] : kFinal;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) w[q] = v[q] < kCross ? jt[v[q]] : kFinal;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) sv[q] = (v[q] < kCross && w[q] == kFinal) ? span[v[q]] : 0u;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (v[q] < kCross) {
+                        const int32_t i = g + q * (int32_t)kWave;
+                        if (w[q] == kFinal) {
+                            span[i] = (uint8_t)sv[q];
+                            jt[i] = kFinal;
+                        } else {
+                            jt[i] = (uint16_t)w[q];
+                            more |= w[q] < kCross;
+                        }
+                    }
+                }
+            }
+            wave_fence();
+            if (!ballot(more)) break;
+        }
+    }
+    st.lap(kStamps, kStRounds);
+    // cross bytes: batches j-1 and j-2 are final once `resolved` reaches j
+    if (!spin<kStamps>(S, [&] { return lds_acquire(&S.resolved) >= j; }, st, kStPrev)) return false;
+    if (ballot(has_cross)) {
+        const int32_t lo1 = hdr[kHdrLo1], lo2 = hdr[kHdrLo2];
+        const lu8* p1 = (const lu8*)S.span[(uint32_t)(j + kPipeSpans - 1) % kPipeSpans] - (lo1 & ~15);
+        const lu8* p2 = (const lu8*)S.span[(uint32_t)(j + kPipeSpans - 2) % kPipeSpans] - (lo2 & ~15);
+        for (int32_t g = i0 + (int32_t)lane; g < s1; g += 4 * kWave) {
+            uint32_t v[4], x[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int32_t i = g + q * (int32_t)kWave;
+                v[q] = i < s1 ? jt[i] : kFinal;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int32_t y = F + (int32_t)(v[q] - kCross);
+                x[q] = (v[q] != kFinal && v[q] >= kCross) ? (y >= lo1 ? p1[y] : p2[y]) : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (v[q] != kFinal && v[q] >= kCross) span[g + q * (int32_t)kWave] = (uint8_t)x[q];
+        }
+        wave_fence();
+    }
+    lds_release(&S.resolved, j + 1);
+    st.lap(kStamps, kStGather);
+    // store pass: 16-byte HBM chunks of [lo, hi); partial end chunks by bytes
+    const int32_t nch = (hi - a0 + 15) >> 4;
+    for (int32_t i = (int32_t)lane; i < nch; i += kWave) {
+        const int32_t c0 = a0 + 16 * i;
+        const lu8* sc = span + 16 * i;
+        if (c0 >= lo && c0 + 16 <= hi) {
+            const u32x4 v = *(const lu128*)sc;
+            stg16(gout + c0, make_uint4(v.x, v.y, v.z, v.w));
+        } else {
+#pragma clang loop unroll(disable) vectorize(disable)
+            for (int32_t x = c0 > lo ? c0 : lo; x < c0 + 16 && x < hi; ++x)
+                *(gu8*)(gout + x) = sc[x - c0];
+        }
+    }
+    st.lap(kStamps, kStSpass);
+    if (!spin<kStamps>(S, [&] { return lds_acquire(&S.stored) >= lo; }, st, kStStore)) return false;
+    stores_done();
+    lds_release(&S.stored, hi);
+    st.lap(kStamps, kStVm);
+    return true;
+}
+
+// 6 workgroups (24 waves) per CU: 80 VGPRs and 19 KiB of LDS each.
+template <bool kStamps>
+__global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
+    const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
+    uint64_t* __restrict__ dbg) {
+    __shared__ __attribute__((aligned(16))) PipeLds S;
     const uint32_t b = blockIdx.x;
     if (b >= nblocks) return;
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
     const int32_t srcSize = src_len[b];
     const int32_t outSize = dst_cap[b];
     const uint8_t* in = src + src_off[b];
     uint8_t* gout = dst + dst_off[b];
     if (special_case(in, srcSize, outSize, ret + b, tid)) return;
-    if (outSize > (int32_t)kOutMax) {
-        wg_fallback(L, in, srcSize, gout, outSize, ret + b, tid);
-        return;
+    if (tid < kPipeRecs) {
+        S.pub[tid] = -1;
+        S.con[tid] = (int32_t)tid - (int32_t)kPipeRecs;
     }
-    const int32_t iend = srcSize, oend = outSize;
-    int32_t ip0 = 0, op = 0;
-    bool fallback = false, done = false;
+    if (tid == 0) {
+        S.nb_total = INT32_MAX;
+        S.resolved = 0;
+        S.stored = 0;
+        S.abort = 0;
+    }
+    __syncthreads();
+    PipeStamps st;
+    if (kStamps) st.t = clock64();
 
-    while (!done) {
-        // ---- stage the window, speculative next-token table --------------
-        for (uint32_t i = tid; i < kWin + kWinPad; i += kWgT) {
-            const int32_t q = ip0 + (int32_t)i;
-            L.win[i] = q < srcSize ? in[q] : 0;
-        }
-        if (tid == 0) L.st[5] = 0;  // long literal runs of this batch
-        __syncthreads();
-        const WinSrc S{L.win, (gcu8*)in, srcSize, ip0};
-#pragma unroll
-        for (uint32_t k = 0; k < kWin / kWgT; ++k) {
-            const uint32_t r = tid + k * kWgT;
-            L.u.j.a[r] = ip0 + (int32_t)r < srcSize ? jump1(L.win, r) : kNone;
-            L.mark[r] = r == 0;
-        }
-        __syncthreads();
-        stp.lap(on, 0);
-        if (on) stp.batches++;
-        // ---- the true token chain: doubling + marking --------------------
-        {
-            uint16_t* A = L.u.j.a;
-            uint16_t* B = L.u.j.b;
-            for (uint32_t lev = 0; lev < kLevels; ++lev) {
-                uint16_t nb[kWin / kWgT];
-#pragma unroll
-                for (uint32_t k = 0; k < kWin / kWgT; ++k) {
-                    const uint32_t r = tid + k * kWgT;
-                    const uint16_t a = A[r];
-                    nb[k] = kNone;
-                    if (a != kNone) {
-                        if (L.mark[r]) L.mark[a] = 1;  // racy reads only add true tokens
-                        nb[k] = A[a];
-                    }
-                }
-                __syncthreads();
-                if (lev + 1 < kLevels) {
-#pragma unroll
-                    for (uint32_t k = 0; k < kWin / kWgT; ++k) B[tid + k * kWgT] = nb[k];
-                    __syncthreads();
-                    uint16_t* t = A;
-                    A = B;
-                    B = t;
-                }
+    if (wave == 0) {
+        // ---------------- parser ----------------
+        Parse P;
+        P.init(in, srcSize, outSize, (lu32*)S.ring, lane);
+        int32_t j = 0, lo1 = 0, lo2 = 0, hi1 = 0, hi2 = 0;
+        bool hbm1 = false, hbm2 = false;
+        for (;;) {
+            Batch bt;
+            const int32_t lo = P.op;
+            const ParseResult pr = parse_batch(P, bt, lane, kPipeOut);
+            st.lap(kStamps, kStParse);
+            if (pr == kParseFail) {
+                if (lane == 0) ret[b] = -P.ip - 1;
+                break;
             }
-        }
-        stp.lap(on, 1);
-        // ---- tokens: rank, output position, the reference's checks --------
-        const uint32_t mk = *reinterpret_cast<const uint32_t*>(&L.mark[4 * tid]);
-        Tok tk[4];
-        uint32_t cnt = 0, osz = 0;
+            // far line: sources before it are read from HBM (see copy_fast)
+            int32_t F = j >= 2 ? lo2 : 0;
+            if (j >= 2 && hbm2) F = F > hi2 ? F : hi2;
+            if (j >= 1 && hbm1) F = F > hi1 ? F : hi1;
+            const uint32_t slot = (uint32_t)j % kPipeRecs;
+            if (!wait_for(S, [&] { return lds_acquire(&S.con[slot]) == j - (int32_t)kPipeRecs; })) {
+                if (lane == 0) ret[b] = kPipeAbort;
+                break;
+            }
+            st.lap(kStamps, kStPWait);
+            S.rec[slot][0][lane] = bt.ls;
+            S.rec[slot][1][lane] = bt.L;
+            S.rec[slot][2][lane] = bt.op;
+            S.rec[slot][3][lane] = bt.off;
+            S.rec[slot][4][lane] = bt.M;
+            if (lane < kHdrWords) {
+                const int32_t h[kHdrWords] = {(int32_t)bt.n, pr == kParsedScalar ? kKindHbm : kKindFast,
+                                              lo, P.op, F, lo1, lo2, 0};
+                int32_t v = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            if ((mk >> (8 * q)) & 0xFF) {
-                tk[q] = parse_tok(S, ip0 + (int32_t)(4 * tid + q));
-                const bool fin = (int64_t)tk[q].lit + tk[q].len == iend;
-                cnt++;
-                osz += tk[q].len + (fin ? 0u : tk[q].m4);
-                if (osz > kLenCap) osz = kLenCap;  // malformed: caught by the checks
+                for (uint32_t q = 0; q < kHdrWords; ++q) v = lane == q ? h[q] : v;
+                S.hdr[slot][lane] = v;
+            }
+            lds_release(&S.pub[slot], j);
+            lo2 = lo1;
+            hi2 = hi1;
+            hbm2 = hbm1;
+            lo1 = lo;
+            hi1 = P.op;
+            hbm1 = pr == kParsedScalar;
+            j++;
+            if (P.done) {
+                if (lane == 0) ret[b] = P.op;
+                break;
             }
         }
-        uint32_t rank, obase, nseq, osum;
-        wg_scan2(cnt, osz, L.red, tid, rank, obase, nseq, osum);
-        bool bad = false, fin_here = false;
-        int32_t o = op + (int32_t)obase;
+        lds_release(&S.nb_total, j);
+        st.lap(kStamps, kStParse);
+    } else {
+        // ---------------- copiers ----------------
+        const uint32_t c = wave - 1;
+        for (int32_t j = (int32_t)c;; j += kCopiers) {
+            const uint32_t slot = (uint32_t)j % kPipeRecs;
+            st.lap(kStamps, kStWork);
+            const bool ok = wait_for(S, [&] {
+                return lds_acquire(&S.pub[slot]) == j || lds_acquire(&S.nb_total) <= j;
+            });
+            st.lap(kStamps, kStRec);
+            if (!ok) {
+                if (lane == 0) ret[b] = kPipeAbort;
+                break;
+            }
+            if (lds_acquire(&S.pub[slot]) != j) break;  // the parser ended before batch j
+            Batch bt;
+            bt.ls = S.rec[slot][0][lane];
+            bt.L = S.rec[slot][1][lane];
+            bt.op = S.rec[slot][2][lane];
+            bt.off = S.rec[slot][3][lane];
+            bt.M = S.rec[slot][4][lane];
+            int32_t hdr[kHdrWords];
 #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            if (!((mk >> (8 * q)) & 0xFF)) continue;
-            const Tok& k = tk[q];
-            const int32_t t = ip0 + (int32_t)(4 * tid + q);
-            const uint32_t Lnib = k.token >> 4, Mnib = k.token & 15;
-            const int64_t litEnd = (int64_t)k.lit + k.len;
-            const bool fin = litEnd == iend;
-            // the two-stage shortcut's entry (:150-155)
-            const bool sc = Lnib != 15 && t + 1 < iend - 16 && o <= oend - 32;
-            // literal-length varint read exactly as the reference's bounded loop (:194-220)
-            const bool lext = Lnib != 15 || (int64_t)k.lit <= (int64_t)iend - 15;
-            bool ok;
-            if (fin) {
-                // final literal run (:223-288): not on the shortcut, fits the output
-                ok = !sc && lext && (int64_t)o + k.len <= oend;
-                fin_here = true;
-            } else {
-                const int64_t mo = (int64_t)o + k.len;  // match start
-                // _copy_match (:298-336, :422-431): offset inside the output,
-                // extension bytes before iend - 5, match end before oend - 5
-                const bool cm = (int64_t)k.off <= mo &&
-                                (Mnib != 15 || (int64_t)k.xm <= (int64_t)iend - 5) &&
-                                mo + k.m4 <= (int64_t)oend - 5;
-                if (sc) ok = (Mnib != 15 && k.off >= 8 && (int64_t)k.off <= mo) || cm;
-                else ok = lext && mo <= (int64_t)oend - 12 && litEnd <= (int64_t)iend - 8 && cm;
-                ok = ok && (int64_t)k.xm < iend;  // the next token exists
-            }
-            bad |= !ok;
-            if (rank < kMaxSeq) {
-                L.s_op[rank] = (uint32_t)o;
-                L.s_lit[rank] = k.lit;
-                L.s_len[rank] = k.len;
-                L.s_off[rank] = k.off;
-                L.s_m4[rank] = fin ? 0u : k.m4;
-                if (k.len > kLongLit) {
-                    const uint32_t li = atomicAdd((uint32_t*)&L.st[5], 1u);
-                    if (li < kMaxLong) L.longs[li] = rank;
-                    else bad = true;
+            for (uint32_t q = 0; q < kHdrWords; ++q) hdr[q] = (int32_t)uni((uint32_t)S.hdr[slot][q]);
+            bt.n = (uint32_t)hdr[kHdrN];
+            lds_release(&S.con[slot], j);
+            if (kStamps) st.acc[kStBatches]++;
+            if (hdr[kHdrKind] == kKindHbm) {
+                // every earlier batch in HBM, then in place
+                if (!spin<kStamps>(S, [&] { return lds_acquire(&S.stored) >= hdr[kHdrLo]; }, st,
+                                   kStStore)) {
+                    if (lane == 0) ret[b] = kPipeAbort;
+                    break;
                 }
-            } else {
-                bad = true;
-            }
-            if (rank + 1 == nseq) {  // the batch's last token: where the next batch starts
-                L.st[0] = (int32_t)k.xm;
-                L.st[1] = fin;
-            }
-            o += (int32_t)(k.len + (fin ? 0u : k.m4));
-            rank++;
-        }
-        bad = __syncthreads_or(bad ? 1 : 0) != 0 || nseq == 0;
-        const bool any_fin = __syncthreads_or(fin_here ? 1 : 0) != 0;
-        if (bad || (any_fin && !L.st[1])) {
-            fallback = true;
-            break;
-        }
-        stp.lap(on, 2);
-        const int32_t op_b = op, op_e = op + (int32_t)osum;
-        const int32_t next_ip = L.st[0];
-        const uint32_t nlong = (uint32_t)L.st[5];
-
-        // ---- literals ------------------------------------------------------
-        for (uint32_t i = tid; i < nseq; i += kWgT) {
-            const uint32_t len = L.s_len[i];
-            if (len > 0 && len <= kLongLit) lit_copy(L.out, L.s_op[i], S, L.s_lit[i], len);
-        }
-        for (uint32_t li = 0; li < nlong; ++li) {
-            const uint32_t i = L.longs[li];
-            const uint32_t len = L.s_len[i], o0 = L.s_op[i], lit = L.s_lit[i];
-            for (uint32_t k = 4 * tid; k < len; k += 4 * kWgT) {
-                const uint32_t c = len - k < 4 ? len - k : 4;
-                lit_copy(L.out, o0 + k, S, lit + k, c);
+                copy_scalar_hbm(bt, in, srcSize, gout, outSize, lane);
+                stores_done();
+                lds_release(&S.resolved, j + 1);
+                lds_release(&S.stored, hdr[kHdrHi]);
+                st.lap(kStamps, kStVm);
+            } else if (!copy_fast<kStamps>(S, c, j, bt, hdr, in, srcSize, gout, lane, st)) {
+                if (lane == 0) ret[b] = kPipeAbort;
+                break;
             }
         }
-        __syncthreads();
-        stp.lap(on, 3);
-
-        // ---- matches, 2 KiB sub-spans -----------------------------------------
-        for (int32_t a = op_b; a < op_e; a += (int32_t)kSub) {
-            const int32_t span = op_e - a < (int32_t)kSub ? op_e - a : (int32_t)kSub;
-            for (uint32_t j = tid; j < kSub; j += kWgT) L.u.ptr[j] = 0;
-            __syncthreads();
-            if (tid == 0) {
-                // the sequence covering a: last one starting at or before it
-                uint32_t lo = 0, hi = nseq - 1;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi + 1) / 2;
-                    if ((int32_t)L.s_op[mid] <= a) lo = mid;
-                    else hi = mid - 1;
-                }
-                L.u.ptr[0] = (uint16_t)(lo + 1);
-            }
-            for (uint32_t i = tid; i < nseq; i += kWgT) {
-                const int32_t so = (int32_t)L.s_op[i];
-                if (so > a && so < a + span) L.u.ptr[so - a] = (uint16_t)(i + 1);
-            }
-            __syncthreads();
-            // byte j = kPer tid + q of the sub-span: its sequence (max scan)
-            constexpr uint32_t kPer = kSub / kWgT;
-            int32_t sid[kPer];
-            int32_t run = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < kPer; ++q) {
-                const int32_t v = L.u.ptr[kPer * tid + q];
-                run = run > v ? run : v;
-                sid[q] = run;
-            }
-            const int32_t pre = wg_excl_max(run, L.red, tid);
-            uint16_t pv[kPer];
-            uint32_t pend = 0;  // my bytes still pointing at an unresolved source
-            uint32_t cs = 0xFFFFFFFFu, c_o = 0, c_len = 0, c_off = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < kPer; ++q) {
-                const int32_t s1 = sid[q] > pre ? sid[q] : pre;
-                const int32_t j = (int32_t)(kPer * tid + q);
-                const int32_t x = a + j;
-                pv[q] = kNone;
-                if (j >= span || s1 == 0) continue;
-                const uint32_t s = (uint32_t)s1 - 1;
-                if (s != cs) {
-                    cs = s;
-                    c_o = L.s_op[s];
-                    c_len = L.s_len[s];
-                    c_off = L.s_off[s];
-                }
-                const int32_t m = (int32_t)(c_o + c_len);
-                if (x < m) continue;  // literal: copied above
-                if (c_off == 0) {     // offset 0 writes zeros (:313, 407-415)
-                    L.out[x] = 0;
-                    continue;
-                }
-                // out[m + t] = out[m - off + t mod off]: the source is before the match
-                const uint32_t t = (uint32_t)(x - m);
-                const int32_t srcp = (t >= c_off) ? m - (int32_t)c_off + (int32_t)(t % c_off)
-                                                  : x - (int32_t)c_off;
-                if (srcp < a) {
-                    L.out[x] = L.out[srcp];  // final: every byte before the sub-span is
-                } else {
-                    pv[q] = (uint16_t)(srcp - a);
-                    pend |= 1u << q;
-                }
-            }
-            __syncthreads();  // every sequence id read before the pointers overwrite them
-#pragma unroll
-            for (uint32_t q = 0; q < kPer; ++q) L.u.ptr[kPer * tid + q] = pv[q];
-            // pointer jumping: a byte whose source is final copies it, the
-            // others jump to their source's source
-            while (__syncthreads_or(pend != 0)) {
-                uint8_t val[kPer];
-                uint32_t got = 0;
-#pragma unroll
-                for (uint32_t q = 0; q < kPer; ++q) {
-                    val[q] = 0;
-                    if (!((pend >> q) & 1)) continue;
-                    const uint16_t py = L.u.ptr[pv[q]];
-                    if (py == kNone) {
-                        val[q] = L.out[a + pv[q]];
-                        got |= 1u << q;
-                    } else {
-                        pv[q] = py;
-                    }
-                }
-                __syncthreads();
-#pragma unroll
-                for (uint32_t q = 0; q < kPer; ++q) {
-                    if (!((pend >> q) & 1)) continue;
-                    const uint32_t j = kPer * tid + q;
-                    if ((got >> q) & 1) {
-                        L.out[a + j] = val[q];
-                        L.u.ptr[j] = kNone;
-                    } else {
-                        L.u.ptr[j] = pv[q];
-                    }
-                }
-                pend &= ~got;
-                if (on) stp.rounds++;
-            }
-        }
-        stp.lap(on, 4);
-        op = op_e;
-        ip0 = next_ip;
-        done = any_fin;
-        __syncthreads();
     }
-    if (fallback) {
-        __syncthreads();
-        wg_fallback(L, in, srcSize, gout, outSize, ret + b, tid);
-        return;
-    }
-    // ---- the image to HBM: 16-byte stores ---------------------------------
-    typedef __attribute__((address_space(1))) uint8_t gu8b;
-    const uint32_t head = (uint32_t)((16 - (reinterpret_cast<uintptr_t>(gout) & 15)) & 15);
-    const uint32_t n = (uint32_t)op;
-    const uint32_t h = head < n ? head : n;
-    for (uint32_t i = tid; i < h; i += kWgT) ((gu8b*)gout)[i] = L.out[i];
-    const uint32_t body = (n - h) & ~15u;
-    for (uint32_t c = h + 16 * tid; c < h + body; c += 16 * kWgT) {
-        const lu8* s = (const lu8*)(L.out + c);
-        stg16(gout + c, make_uint4(ld4(s), ld4(s + 4), ld4(s + 8), ld4(s + 12)));
-    }
-    for (uint32_t i = h + body + tid; i < n; i += kWgT) ((gu8b*)gout)[i] = L.out[i];
-    if (tid == 0) ret[b] = op;
-    if (kStamps) {
-        __syncthreads();
-        stp.lap(on, 5);
-        if (on && dbg) {
-            uint64_t* d = dbg + 8 * (size_t)b;
-            for (int i = 0; i < 6; ++i) d[i] = stp.acc[i];
-            d[6] = stp.batches;
-            d[7] = stp.rounds;
+    if constexpr (kStamps) {
+        if (lane == 0 && dbg) {
+            uint64_t* d = dbg + kStSlots * (size_t)b;
+            for (int k = 0; k < kStSlots; ++k)
+                if (st.acc[k]) atomicAdd((unsigned long long*)(d + k), (unsigned long long)st.acc[k]);
         }
     }
 }
 
+// Blocks whose capacity is at least this take the pipelined decoder (small
+// blocks parse in a few batches; one wave each keeps more of them resident).
+constexpr uint32_t kPipeMinCap = 16384;
+
 template <bool kStamps>
 hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* dbg) {
     if (a.nblocks == 0) return hipSuccess;
-    // LZ4E_DECOMPRESS_WAVE=1 keeps every block on the one-wave decoder (A/B).
-    static const bool wave_only = getenv("LZ4E_DECOMPRESS_WAVE") != nullptr;
-    if (!wave_only && a.max_cap > 0 && a.max_cap <= kOutMax) {
-        hipLaunchKernelGGL((decompress_wg_kernel<kStamps>), dim3(a.nblocks), dim3(kWgT), 0, stream,
-                           a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret,
+    // LZ4E_DECOMPRESS_MODE=wave|pipe overrides the choice (A/B experiments).
+    static const char* env = getenv("LZ4E_DECOMPRESS_MODE");
+    uint32_t mode = a.mode;
+    if (mode == kDecAuto && env) mode = env[0] == 'w' ? kDecWave : (env[0] == 'p' ? kDecPipe : kDecAuto);
+    if (mode == kDecAuto) mode = (a.max_cap == 0 || a.max_cap >= kPipeMinCap) ? kDecPipe : kDecWave;
+    if (mode == kDecPipe) {
+        hipLaunchKernelGGL((decompress_pipe_kernel<kStamps>), dim3(a.nblocks), dim3(kPipeWaves * kWave),
+                           0, stream, a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret,
                            a.nblocks, dbg);
         return hipGetLastError();
     }

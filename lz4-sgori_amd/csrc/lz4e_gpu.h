@@ -35,10 +35,13 @@ struct DecompressBatch {
     const int32_t* dst_cap;
     int32_t* ret;
     uint32_t nblocks;
-    // Upper bound of dst_cap[] (0: unknown).  At most 64 KiB selects the
-    // workgroup decoder (output image in LDS); otherwise one wave per block.
+    // Upper bound of dst_cap[] (0: unknown): blocks of 16 KiB and more (or
+    // unknown) take the pipelined 4-wave decoder, smaller ones one wave each.
     uint32_t max_cap;
+    uint32_t mode = 0;  // kDecAuto, or force kDecWave / kDecPipe (tests, A/B)
 };
+
+enum : uint32_t { kDecAuto = 0, kDecWave = 1, kDecPipe = 2 };
 
 uint32_t compress_lds_bytes(uint32_t max_len, bool lds_input);
 hipError_t launch_compress(const CompressBatch& a, hipStream_t stream);

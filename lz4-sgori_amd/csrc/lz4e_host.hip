@@ -548,15 +548,17 @@ int lz4e_debug_compress_stamped(const uint8_t* src, const uint64_t* src_off, con
                : -1;
 }
 
-// Diagnostic (not part of include/lz4e.h): the decompress kernel with
-// per-block phase cycle counters, 8 x u64 per block into dbg (max_cap as in
-// lz4e_decompress_batch_dev: <= 64 KiB stamps the workgroup decoder).
+// Diagnostic (not part of include/lz4e.h): the decompress kernels with a
+// forced decoder (mode 0 auto, 1 one wave per block, 2 pipelined) and, when
+// dbg is not null, the stamped build's per-block cycle counters (8 x u64 per
+// block, dbg zeroed by the caller).
 int lz4e_debug_decompress_stamped(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
                                   uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
                                   int32_t* ret, uint32_t nblocks, void* stream, uint64_t* dbg,
-                                  uint32_t max_cap) {
-    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap};
-    return hip_ok(lz4e::launch_decompress_stamped(a, static_cast<hipStream_t>(stream), dbg),
+                                  uint32_t max_cap, uint32_t mode) {
+    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap, mode};
+    const hipStream_t s = static_cast<hipStream_t>(stream);
+    return hip_ok(dbg ? lz4e::launch_decompress_stamped(a, s, dbg) : lz4e::launch_decompress(a, s),
                   "decompress launch")
                ? 0
                : -1;

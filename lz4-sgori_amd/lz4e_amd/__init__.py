@@ -425,7 +425,8 @@ def decompress_batch_dev(src, src_off, src_len, dst, dst_off, dst_cap, ret, stre
     """lz4e_decompress_batch_dev on torch tensors (launch only).
 
     ``max_cap`` bounds dst_cap (default: read from it, which synchronises);
-    up to 65536 selects the workgroup decoder."""
+    16 KiB and more selects the pipelined 4-wave decoder, smaller blocks
+    decode on one wave each."""
     import torch
     n = int(src_len.numel())
     if max_cap is None:

@@ -72,7 +72,12 @@ def _gpu_compress(amd, blocks, ttypes, caps=None):
     return r, frames, ax
 
 
-def _gpu_decompress(amd, frames, caps, csizes=None, max_cap=None):
+DEC_AUTO, DEC_WAVE, DEC_PIPE = 0, 1, 2
+
+
+def _gpu_decompress(amd, frames, caps, csizes=None, max_cap=None, mode=DEC_AUTO):
+    """Decode on the GPU; mode forces a decoder (one wave per block, or the
+    pipelined 4-wave one) through the diagnostic entry point."""
     import torch
     n = len(frames)
     csizes = [len(f) for f in frames] if csizes is None else csizes
@@ -91,8 +96,18 @@ def _gpu_decompress(amd, frames, caps, csizes=None, max_cap=None):
     src = torch.from_numpy(host).to(dev)
     dst = torch.zeros(int(doffs[-1] + slot[-1]) + 16, dtype=torch.uint8, device=dev)
     ret = torch.full((n,), -7777, dtype=torch.int32, device=dev)
-    amd.decompress_batch_dev(src, t(offs, np.int64), t(csizes, np.int32), dst, t(doffs, np.int64),
-                             t(caps, np.int32), ret, max_cap=max_cap)
+    if mode == DEC_AUTO:
+        amd.decompress_batch_dev(src, t(offs, np.int64), t(csizes, np.int32), dst, t(doffs, np.int64),
+                                 t(caps, np.int32), ret, max_cap=max_cap)
+    else:
+        L = amd.lib()
+        P = ctypes.c_void_p
+        L.lz4e_debug_decompress_stamped.argtypes = [P] * 7 + [ctypes.c_uint32, P, P, ctypes.c_uint32,
+                                                               ctypes.c_uint32]
+        a = [t(offs, np.int64), t(csizes, np.int32), t(doffs, np.int64), t(caps, np.int32)]
+        assert L.lz4e_debug_decompress_stamped(src.data_ptr(), a[0].data_ptr(), a[1].data_ptr(),
+                                               dst.data_ptr(), a[2].data_ptr(), a[3].data_ptr(),
+                                               ret.data_ptr(), n, None, None, 0, mode) == 0
     torch.cuda.synchronize()
     r = ret.cpu().numpy()
     d = dst.cpu().numpy()
@@ -326,14 +341,15 @@ def test_full_size_roundtrip(gpu, cls, bs, kind):
         assert frames[i] == oracle_ref.compress(blocks[i], cls)[1]
 
 
+@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE], ids=["wave", "pipe"])
 @pytest.mark.parametrize("cap_extra", [0, 100000])
-def test_decompress_periodic_matches(gpu, cap_extra):
+def test_decompress_periodic_matches(gpu, cap_extra, mode):
     """Self-overlapping matches of every period 1..40 and lengths around
-    1x-3x the period (the overlap-copy cases).  With the exact capacity the
-    last sequences fall inside the reference's end-of-output margins
-    (op > oend - 32 / oend - 12: no shortcut, exact end checks,
-    lz4e_decompress.c:150-191, 223-288, 422-431); with 100 KB spare every
-    sequence stays on the fast path."""
+    1x-3x the period (the overlap-copy cases), on both decoders.  With the
+    exact capacity the last sequences fall inside the reference's
+    end-of-output margins (op > oend - 32 / oend - 12: no shortcut, exact end
+    checks, lz4e_decompress.c:150-191, 223-288, 422-431) and take the scalar
+    path; with 100 KB spare they stay on the fast path (span-staged)."""
     rng = np.random.default_rng(99)
     frames, caps, expect = [], [], []
     for period in range(1, 41):
@@ -346,7 +362,7 @@ def test_decompress_periodic_matches(gpu, cap_extra):
         frames.append(oracle_ref.compress(b, BYU16)[1])
         caps.append(len(b) + cap_extra)
         expect.append(b)
-    r, outs = _gpu_decompress(gpu, frames, caps)
+    r, outs = _gpu_decompress(gpu, frames, caps, mode=mode)
     for i in range(len(frames)):
         assert r[i] == len(expect[i]), i
         assert outs[i] == expect[i], i
@@ -620,12 +636,10 @@ def test_full_size_every_frame(gpu, name):
 
 
 @pytest.mark.parametrize("kind", ["mixed", "text", "runs", "ints", "random", "small_alpha", "fio"])
-def test_decompress_workgroup_vs_wave_decoder(gpu, kind):
-    """The two decoders on the same frames -- the workgroup decoder (LDS image,
-    max_cap <= 64 KiB) and the one-wave decoder (max_cap = 0) -- valid frames,
-    exact and spare capacities, and corrupted ones (the workgroup decoder's
-    checks hand those to the exact path): identical values and bytes, both
-    equal to the oracle's."""
+def test_decompress_pipelined_vs_wave_decoder(gpu, kind):
+    """The two decoders on the same frames -- the pipelined 4-wave decoder and
+    the one-wave decoder -- valid frames, exact and spare capacities, and
+    corrupted ones: identical values and bytes, both equal to the oracle's."""
     rng = np.random.default_rng(zlib.crc32(kind.encode()))
     data = _corpus(kind, 1 << 20, 31)
     frames, caps, want = [], [], []
@@ -650,8 +664,8 @@ def test_decompress_workgroup_vs_wave_decoder(gpu, kind):
         frames.append(f)
         caps.append(cap)
         want.append(oracle_ref.decompress(f, cap))
-    r_wg, o_wg = _gpu_decompress(gpu, frames, caps, max_cap=65536)
-    r_wv, o_wv = _gpu_decompress(gpu, frames, caps, max_cap=0)
+    r_wg, o_wg = _gpu_decompress(gpu, frames, caps, mode=DEC_PIPE)
+    r_wv, o_wv = _gpu_decompress(gpu, frames, caps, mode=DEC_WAVE)
     for i, (er, eb) in enumerate(want):
         assert r_wg[i] == er == r_wv[i], (i, r_wg[i], er, r_wv[i])
         if er >= 0:

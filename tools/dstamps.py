@@ -19,7 +19,7 @@ import lz4e_amd  # noqa
 from lz4e_amd import corpus  # noqa
 L = lz4e_amd.lib()
 P = ctypes.c_void_p
-L.lz4e_debug_decompress_stamped.argtypes = [P] * 7 + [ctypes.c_uint32, P, P, ctypes.c_uint32]
+L.lz4e_debug_decompress_stamped.argtypes = [P] * 7 + [ctypes.c_uint32, P, P, ctypes.c_uint32, ctypes.c_uint32]
 
 def run(name, data, bs, cls):
     dev = torch.device("cuda")
@@ -42,7 +42,7 @@ def run(name, data, bs, cls):
     for _ in range(2):
         assert L.lz4e_debug_decompress_stamped(dst.data_ptr(), doffs.data_ptr(), ret.data_ptr(), out.data_ptr(),
                                                offs.data_ptr(), lens.data_ptr(), dret.data_ptr(), n, s,
-                                               dbg.data_ptr(), 0) == 0
+                                               dbg.data_ptr(), 0, 1) == 0
     torch.cuda.synchronize()
     assert torch.equal(out[:n * bs], src)
     d = dbg.cpu().numpy().reshape(n, 8).astype(np.float64)
