@@ -565,13 +565,33 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                                 chain_tables(vc, vm, vb, fc, fe, jv);
                             }
                             if (kStamps) st.lap(kPhCount);
+                            // The serial part: the chain from ks.  fc^2, fc^3
+                            // and fc^4 (a lane past the window or stopped stays
+                            // put) let one step read four links with independent
+                            // readlanes instead of one dependent readlane each.
+                            // (every lane takes part in each shuffle)
+                            const uint32_t g1 = shfl(fc, fc & 63);
+                            const uint32_t J2 = fc < 64 ? g1 : fc;
+                            const uint32_t g2 = shfl(fc, J2 & 63), g3 = shfl(J2, J2 & 63);
+                            const uint32_t J3 = J2 < 64 ? g2 : J2;
+                            const uint32_t J4 = J2 < 64 ? g3 : J2;
                             k = ks;
                             evm = 0;
-                            while (k < 64) {  // the serial part: one readlane per event
-                                const uint32_t w = lane_val(fc, k);
-                                if (w & kStop) break;
+                            while (k < 64) {
+                                const uint32_t x1 = lane_val(fc, k), x2 = lane_val(J2, k);
+                                const uint32_t x3 = lane_val(J3, k), x4 = lane_val(J4, k);
+                                if (x1 & kStop) break;
                                 evm |= 1ull << k;
-                                k = w;
+                                if (x1 >= 64) { k = x1; break; }
+                                if (x2 & kStop) { k = x1; break; }
+                                evm |= 1ull << x1;
+                                if (x2 >= 64) { k = x2; break; }
+                                if (x3 & kStop) { k = x2; break; }
+                                evm |= 1ull << x2;
+                                if (x3 >= 64) { k = x3; break; }
+                                if (x4 & kStop) { k = x3; break; }
+                                evm |= 1ull << x3;
+                                k = x4;
                             }
                             nev = popc64(evm);
                             // the chain's puts (e-2 and e of every event, the probes

@@ -66,9 +66,18 @@ def run(name, data, bs, cls, label):
     for i, p in enumerate(ph):
         print(f"   {p:8s} {d[:, i].mean():12.0f}  ({100 * d[:, i].sum() / tot.sum():5.1f}%)")
     by_class(name, tot, n, lambda m: f"seq {seqs[m].mean():.0f} win {srch[m].mean():.0f} pass {rem[m].mean():.0f} att {fa[m].mean():.0f} fseq {fev[m].mean():.0f} " + " ".join(f"{ph[i]}={d[m, i].mean():.0f}" for i in range(6)))
+    if name.startswith("silesia"):
+        cls = np.random.default_rng(0x5157).choice(6, size=n, p=[0.40, 0.15, 0.10, 0.10, 0.10, 0.15])
+        top = np.argsort(-tot)[:12]
+        print("   slowest blocks: " + ", ".join(f"{i}:{CLASS_NAMES[cls[i]]}:{tot[i] / 1e6:.2f}M" for i in top))
+        for i in top[:4]:
+            blk = data[i * bs:(i + 1) * bs]
+            print(f"   block {i}: " + " ".join(f"{ph[k]}={d[i, k] / 1e6:.2f}M" for k in range(6)) +
+                  f" seq {seqs[i]} win {srch[i]} pass {rem[i]} ratio {bs / max(1, int(ret[i])):.2f}"
+                  f" head {bytes(blk[:24]).hex()}")
 
 if __name__ == "__main__":
     mode = os.environ.get("LZ4E_COMPRESS_LDS_MAX", "default")
-    run("silesia64k", corpus.silesia_proxy(1024 * 65536, 0x5157), 65536, 1, f"lds_max={mode}")
+    run("silesia64k", corpus.silesia_proxy(3234 * 65536, 0x5157), 65536, 1, f"lds_max={mode}")
     run("text64k", corpus.text_proxy(512 * 65536, 7), 65536, 1, f"lds_max={mode}")
     run("fio4k", corpus.fio_pattern(16384 * 4096), 4096, 1, f"lds_max={mode}")
