@@ -31,16 +31,16 @@ def main():
     write = per_kernel(os.path.join(prof, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     res = json.load(open(out)) if os.path.exists(out) else {}
     ent = {}
-    for k in ("compress_kernel", "decompress_kernel"):
+    for k, d in (("compress_kernel", "compress"), ("decompress_pipe_kernel", "decompress"),
+                 ("decompress_kernel", "decompress")):
         name = next((n for n in fetch if n.startswith(k)), None)
-        if name is None:
+        if name is None or d in ent:
             continue
         f_raw = fetch[name] * 1024
         w = write.get(name, 0.0) * 1024
-        d = k.replace("_kernel", "")
         ent[d] = round(2 * f_raw + w)
-        ent[d + "_detail"] = {"fetch_bytes_raw": round(f_raw), "fetch_bytes_x2": round(2 * f_raw),
-                              "write_bytes": round(w)}
+        ent[d + "_detail"] = {"kernel": k, "fetch_bytes_raw": round(f_raw),
+                              "fetch_bytes_x2": round(2 * f_raw), "write_bytes": round(w)}
     ent["source"] = prof
     res[workload] = ent
     json.dump(res, open(out, "w"), indent=1)
