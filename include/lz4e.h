@@ -210,6 +210,65 @@ int lz4e_decompress_batch_dev(const uint8_t *src, const uint64_t *src_off,
 			      void *stream);
 
 /*
+ * Dictionary mode.  The reference stubs its dictionary
+ * path out (lz4e/lz4e_compress.c:250-266, 315-324, 393-419, 472-482; the
+ * dictionary fields of LZ4E_stream_t, lz4e/include/lz4e.h:36-40) and its
+ * exported decoder never instantiates the extDict branches
+ * (lz4e/lz4e_decompress.c:299-302, 339-378, 462-469).  This is the LZ4E
+ * extension built on them; no reference run pins its frames (parity
+ * unpinned), the decoder restates those branches exactly.
+ *
+ * LZ4E_compress_usingDict: LZ4E_compress_default's contract (bio_vec source
+ * and destination, iterators, wrkmem) compressing against the last <= 64 KiB
+ * of `dictionary` (ignored under 8 bytes): the hash table is preloaded the
+ * way LZ4_loadDict does it (every third dictionary position, in order), the
+ * table class is byU32 whatever the SG layout, and matches may start in the
+ * dictionary (offsets <= LZ4E_DISTANCE_MAX) and run on into the block.  The
+ * >256-segment and size limits of LZ4E_compress_default still return 0.
+ *
+ * LZ4E_decompress_safe_usingDict: LZ4E_decompress_safe with a dictionary that
+ * logically precedes `dest` (extDict): match bytes before `dest` read the
+ * dictionary's end; with dictSize < 64 KiB an offset reaching before the
+ * dictionary fails (-(ip - src) - 1, :299-302).  dictSize 0 is
+ * LZ4E_decompress_safe.  Frames of LZ4E_compress_usingDict decode with the
+ * same dictionary, so do those of any LZ4 dictionary compressor.
+ */
+int LZ4E_compress_usingDict(const struct bio_vec *src, struct bio_vec *dst,
+			    struct bvec_iter *srcIter, struct bvec_iter *dstIter,
+			    void *wrkmem, const char *dictionary, int dictSize);
+int LZ4E_decompress_safe_usingDict(const char *source, char *dest,
+				   int compressedSize, int maxDecompressedSize,
+				   const char *dictStart, int dictSize);
+
+/* Batch forms: request i with dictionary (dicts[i], dict_sizes[i]) (NULL or
+ * size 0: none, still byU32 on the compress side); returns as the
+ * dictionary-less batch calls. */
+int lz4e_compress_sg_batch_dict(struct lz4e_sg_request *reqs, int n,
+				const char *const *dicts, const int *dict_sizes);
+int lz4e_decompress_batch_dict(const char *const *src, const int *csize,
+			       char *const *dst, const int *cap,
+			       const char *const *dicts, const int *dict_sizes,
+			       int *ret, int n);
+
+/* Device-resident dictionary batches: block i's dictionary is the
+ * dict_len[i] bytes right before its input (compress: src + src_off[i],
+ * table_type[i] must be 3 = byU32; at most 64 KiB used) or right before its
+ * output (decompress: dst + dst_off[i] -- e.g. the previous block of the
+ * same stream decoded in place, so a stream decodes block after block while
+ * many streams decode in parallel). */
+int lz4e_compress_batch_dev_dict(const uint8_t *src, const uint64_t *src_off,
+				 const uint32_t *src_len, const uint8_t *table_type,
+				 uint8_t *dst, const uint64_t *dst_off,
+				 const uint32_t *dst_cap, int32_t *ret, uint32_t *aux,
+				 uint32_t nblocks, uint32_t max_len,
+				 const uint32_t *dict_len, void *stream);
+int lz4e_decompress_batch_dev_dict(const uint8_t *src, const uint64_t *src_off,
+				   const int32_t *src_len, uint8_t *dst,
+				   const uint64_t *dst_off, const int32_t *dst_cap,
+				   int32_t *ret, uint32_t nblocks, uint32_t max_cap,
+				   const int32_t *dict_len, void *stream);
+
+/*
  * LZ4E_decompress_safe into a bio_vec list (the read
  * side without a bounce buffer).  Decodes compressedSize bytes at `source`
  * into the segments of `dst` from *dstIter on, with capacity

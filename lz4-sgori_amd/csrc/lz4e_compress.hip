@@ -347,19 +347,29 @@ LZ4E_DEV uint64_t lane_range(uint32_t a, uint32_t b) {
 // The window's puts are written to the table once, when the walk leaves it.
 template <int TT, bool kStamps, class IMG>
 LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* out, uint32_t cap,
-                             int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg, uint32_t lane) {
+                             int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg, uint32_t lane,
+                             uint32_t D = 0) {
+    // Dictionary mode (D > 0): the image is [D dictionary bytes | the n-byte
+    // block], the parse starts at D and the table was preloaded from the
+    // dictionary; positions are image positions throughout.
     const Table<TT> T{smem};
     const uint64_t bound = (uint64_t)n + n / 255 + 16;
     const bool limited = cap < bound;  // lz4e_compress.c:553-560
-    uint32_t op = 0, anchor = 0, ip = 0;
+    uint32_t op = 0, anchor = D, ip = D;
     [[maybe_unused]] uint32_t trn = 0;
     Stamps st;
     if (kStamps) st.start();
 
     if (n >= kMinLength) {
-        const uint32_t mflimit = n - kMfLimit;
-        const uint32_t matchlimit = n - kLastLiterals;
+        const uint32_t mflimit = D + n - kMfLimit;
+        const uint32_t matchlimit = D + n - kLastLiterals;
         const uint64_t lanes_below = (1ull << lane) - 1;
+        // First byte (lz4e_compress.c:280-282): put(D); in noDict mode that is
+        // position 0 into a zeroed table, a no-op.
+        if (D != 0) {
+            if (lane == 0) T.put(hash_val<TT>(img.ld64(D)), D);
+            lockstep();
+        }
 
         // ---- sequence output -------------------------------------------
         // offset, match-length code and token of a sequence whose token slot
@@ -391,8 +401,8 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
         };
 
         bool rmode = false;  // e is a match end (rematch) / the next probe of a search
-        uint32_t e = 1;      // next position of the walk
-        uint32_t s = 1;      // start of the current search
+        uint32_t e = D + 1;  // next position of the walk
+        uint32_t s = D + 1;  // start of the current search
         uint32_t jb = 0;     // probes of the current search done so far
         uint32_t pf = 0;     // prefetch of the next window's bytes (warms L1/L2)
         // Large blocks only: a batch's kernel time is its slowest block, and
@@ -402,7 +412,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
         for (;;) {
             // ================= window setup =================================
             if (prio_q != 5) {
-                const uint32_t q = (uint32_t)(((uint64_t)e * 4) / n);
+                const uint32_t q = (uint32_t)(((uint64_t)(e - D) * 4) / n);
                 if (q != prio_q) {
                     prio_q = q;
                     wave_prio_for(q);
@@ -939,7 +949,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
 
 last_literals: {
         // lz4e_compress.c:500-530
-        const uint32_t R = n - anchor;
+        const uint32_t R = D + n - anchor;
         if (limited && (uint64_t)op + R + 1 + (R + 240) / 255 > cap) goto fail;
         if (R >= 15) {
             if (lane == 0) out[op] = 0xF0;
@@ -953,7 +963,7 @@ last_literals: {
         if (lane == 0) {
             *ret_slot = (int32_t)(op + R);
             if (aux_slot) {
-                aux_slot[0] = ip;
+                aux_slot[0] = ip - D;
                 aux_slot[1] = R;
             }
         }
@@ -1009,9 +1019,9 @@ LZ4E_DEV void stage_block(uint32_t* dstw, const uint8_t* src, uint32_t n, uint32
 template <bool kStamps, class IMG>
 LZ4E_DEV void dispatch_class(const IMG& img, uint32_t* smem, uint32_t n, int tt, gu8* out,
                              uint32_t cap, int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg,
-                             uint32_t lane) {
+                             uint32_t lane, uint32_t D = 0) {
     if (tt == kByU32)
-        compress_block<kByU32, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane);
+        compress_block<kByU32, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, D);
     else if (tt == kByU16)
         compress_block<kByU16, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane);
     else
@@ -1028,7 +1038,8 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
                                                       const uint32_t* __restrict__ dst_cap,
                                                       int32_t* __restrict__ ret,
                                                       uint32_t* __restrict__ aux, uint32_t nblocks,
-                                                      uint32_t max_len, uint64_t* __restrict__ dbg) {
+                                                      uint32_t max_len, uint64_t* __restrict__ dbg,
+                                                      const uint32_t* __restrict__ dict_len) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
     const uint32_t b = blockIdx.x;
     if (b >= nblocks) return;
@@ -1041,10 +1052,15 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
     uint32_t* aux_slot = aux ? aux + 2 * (size_t)b : nullptr;
     uint64_t* dbg_slot = dbg ? dbg + 8 * (size_t)b : nullptr;
 
+    // Dictionary mode: the dict_len[b] (<= 64 KiB) bytes before the block
+    // are its dictionary; under 8 bytes it is ignored (LZ4_loadDict:
+    // dictSize < HASH_UNIT).  byU32 only, HBM image only.
+    const uint32_t D = dict_len && dict_len[b] >= 8 ? dict_len[b] : 0;
     const bool tt_ok = (tt == kByU16 && n <= 65536) || tt == kByU32 || tt == kByU64;
+    const bool dict_ok = D == 0 || (tt == kByU32 && D <= 65536 && !kLdsInput);
     // the launch sized LDS (staging mode) for blocks of at most max_len bytes
     const bool fits = !kLdsInput || n <= max_len;
-    if (n > kMaxInput || (n >= kMinLength && !tt_ok) || !fits) {
+    if (n > kMaxInput || (n >= kMinLength && !tt_ok) || !fits || !dict_ok) {
         // Input too large (lz4e_compress.c:245-248) returns 0; a malformed
         // descriptor (class/length the SG rules cannot produce, or a block
         // longer than the batch's max_len) returns -1.
@@ -1066,8 +1082,17 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
         dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane);
     } else {
         block_sync();
-        const HbmImage img{(gcu8*)in, n, buf_make(in, n)};
-        dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane);
+        const uint8_t* base = in - D;
+        const HbmImage img{(gcu8*)base, D + n, buf_make(base, D + n)};
+        if (D != 0 && n >= kMinLength) {
+            // LZ4_loadDict: every third dictionary position p with p + 8 <= D
+            // (HASH_UNIT), in order -- the last put of a hash wins, so the
+            // largest p of each hash (LDS atomic max)
+            for (uint32_t p = 3 * lane; p + 8 <= D; p += 3 * kWave)
+                atomicMax(&smem[hash_val<kByU32>(img.ld64(p))], p);
+            block_sync();
+        }
+        dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane, D);
     }
 }
 
@@ -1081,17 +1106,17 @@ hipError_t launch_compress_impl(const CompressBatch& a, hipStream_t stream, uint
     if (a.nblocks == 0) return hipSuccess;
     // LZ4E_COMPRESS_LDS_MAX (bytes) overrides the LDS staging limit (experiments).
     static const uint32_t lds_max = env_u32("LZ4E_COMPRESS_LDS_MAX", kMaxLdsInput);
-    const bool lds_input = a.max_len <= lds_max;
+    const bool lds_input = a.max_len <= lds_max && a.dict_len == nullptr;
     const dim3 grid(a.nblocks), block(kWave);
     const uint32_t lds = compress_lds_bytes(a.max_len, lds_input);
     if (lds_input) {
         hipLaunchKernelGGL((compress_kernel<true, kStamps>), grid, block, lds, stream, a.src,
                            a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.aux, a.nblocks, a.max_len, dbg);
+                           a.aux, a.nblocks, a.max_len, dbg, a.dict_len);
     } else {
         hipLaunchKernelGGL((compress_kernel<false, kStamps>), grid, block, lds, stream, a.src,
                            a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.aux, a.nblocks, a.max_len, dbg);
+                           a.aux, a.nblocks, a.max_len, dbg, a.dict_len);
     }
     return hipGetLastError();
 }

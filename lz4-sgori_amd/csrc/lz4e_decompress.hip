@@ -100,6 +100,7 @@ struct InWindow {
         put_ring(seg, a);
         put_ring(seg + 1, b);
         ring_lo = base;
+        lockstep();  // other lanes read the ring next
     }
     LZ4E_DEV void slide() {
         a = b;
@@ -110,6 +111,7 @@ struct InWindow {
         c = load(seg * 64 + 128 + (int32_t)lane);
         const int32_t lo = base - 512;  // segments seg-2 .. seg+1 stay in the ring
         ring_lo = ring_lo > lo ? ring_lo : lo;
+        lockstep();  // other lanes read the ring next
     }
     // Byte p of the block (reloads when p is outside [base, base + 512)).
     LZ4E_DEV uint32_t byte(int32_t p) {
@@ -290,15 +292,16 @@ LZ4E_DEV void wave_match(uint8_t* out, int32_t op, uint32_t off, int32_t len, ui
         for (int32_t t = lane; t < len; t += kWave) out[op + t] = 0;
         return;
     }
+    const int32_t src = op - (int32_t)off;  // signed: a dictionary source lies before out
     if (off >= 16 * kWave) {
         // each 1 KiB step reads bytes written before the step
         for (int32_t k0 = 0; k0 < len; k0 += 16 * kWave) {
             const int32_t k = k0 + 16 * (int32_t)lane;
             if (k + 16 <= len) {
                 *reinterpret_cast<uint4*>(out + op + k) =
-                    *reinterpret_cast<const uint4*>(out + op - off + k);
+                    *reinterpret_cast<const uint4*>(out + src + k);
             } else {
-                for (int32_t t = k; t < len && t < k + 16; ++t) out[op + t] = out[op - off + t];
+                for (int32_t t = k; t < len && t < k + 16; ++t) out[op + t] = out[src + t];
             }
             wave_fence();
         }
@@ -308,7 +311,7 @@ LZ4E_DEV void wave_match(uint8_t* out, int32_t op, uint32_t off, int32_t len, ui
     // come from the final period [op-off, op), the rest from P bytes back.
     const int32_t P = (int32_t)off * ((16 * kWave + off - 1) / off);
     const int32_t head = len < P ? len : P;
-    for (int32_t t = lane; t < head; t += kWave) out[op + t] = out[op - off + (t % off)];
+    for (int32_t t = lane; t < head; t += kWave) out[op + t] = out[src + (int32_t)(t % off)];
     wave_fence();
     for (int32_t k0 = P; k0 < len; k0 += 16 * kWave) {
         const int32_t k = k0 + 16 * (int32_t)lane;
@@ -475,10 +478,11 @@ struct Parse {
     InWindow win;
     int32_t iend, oend, shortiend, shortoend;
     int32_t ip, op;
+    int32_t D;  // dictionary bytes before the output (<= 65536; 0: noDict)
     bool done;  // the final literal run has been parsed
 
     LZ4E_DEV void init(const uint8_t* in, int32_t srcSize, int32_t outSize, lu32* ring,
-                       uint32_t lane) {
+                       uint32_t lane, int32_t dict = 0) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(in);
         win.shift = (int32_t)(a & 3);
         win.w = (gcu32*)(a - win.shift);
@@ -492,6 +496,7 @@ struct Parse {
         shortoend = oend - 14 - 18; // :102-103
         ip = 0;
         op = 0;
+        D = dict;
         done = false;
     }
 };
@@ -563,9 +568,12 @@ LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_
         const int32_t m_k = o_k + L;
         // the reference's checks on this path: shortcut entry (op <= oend-32,
         // input side guaranteed by jlim), match inside the block (:299-302),
-        // and for offsets < 8 the _copy_match end check (:422-431)
-        const bool ok = cand && o_k <= oend - 32 && m_k >= off &&
-                        (off >= 8 || m_k + Mt + 4 <= oend - 5) && incl <= cap_out;
+        // and for offsets < 8 the _copy_match end check (:422-431); a source
+        // in the dictionary takes _copy_match: offset inside dictionary +
+        // block (:299-302), then the extDict end check (:341-346)
+        const bool ok = cand && o_k <= oend - 32 && incl <= cap_out &&
+                        (m_k >= off ? (off >= 8 || m_k + Mt + 4 <= oend - 5)
+                                    : (m_k - off + P.D >= 0 && m_k + Mt + 4 <= oend - 5));
         const uint64_t okm = ballot(ok);
         const uint32_t nf = (~okm) ? ctz64(~okm) : kWave;  // first failing lane
         if (nf > 0) {
@@ -638,8 +646,9 @@ LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_
     length = token & 15;
 
 copy_match_checks:
-    // _copy_match (:298-336, :422-431)
-    if (op - offset < 0) goto fail;
+    // _copy_match (:298-336, :422-431); with a dictionary the source may lie
+    // up to D bytes before the output (:299-302, checkOffset)
+    if (op - offset + P.D < 0) goto fail;
     if (length == 15) {
         uint32_t s;
         do {
@@ -706,7 +715,7 @@ struct Stamps {
 template <bool kStamps>
 LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, int32_t outSize,
                            int32_t* ret_slot, uint64_t* dbg, uint32_t lane, lu8* span,
-                           lu32* ring, lu16* jump) {
+                           lu32* ring, lu16* jump, int32_t dict) {
     Stamps st;
     auto lap = [&](int ph) {
         if constexpr (kStamps) {
@@ -718,7 +727,7 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
     if constexpr (kStamps) st.t = clock64();
     lu8* sink = (lu8*)ring + kRing + kRingPad + 4 * lane;  // (span follows the sink)
     Parse P;
-    P.init(in, srcSize, outSize, ring, lane);
+    P.init(in, srcSize, outSize, ring, lane, dict);
 
     for (;;) {
         Batch b;
@@ -786,6 +795,7 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
                 if constexpr (kStamps) st.rounds++;
             }
             lap(2);
+            lockstep();  // the last round's span bytes, read by other lanes
             // store pass: 16-byte HBM chunks of [lo, op); partial end chunks by bytes
             const int32_t nch = (op - a0 + 15) >> 4;
             for (int32_t i = (int32_t)lane; i < nch; i += kWave) {
@@ -821,6 +831,15 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
     }
 }
 
+// Dictionary bytes of block b: the dict_len[b] bytes before its output;
+// anything from 64 KiB on behaves alike (no offset reaches further, and the
+// reference's checkOffset is off, :93).
+LZ4E_DEV int32_t dict_of(const int32_t* dict_len, uint32_t b) {
+    if (!dict_len) return 0;
+    const int32_t d = dict_len[b];
+    return d <= 0 ? 0 : (d > 65536 ? 65536 : d);
+}
+
 // The reference's special cases (lz4e_decompress.c:113-120); true when the
 // block is fully handled.
 LZ4E_DEV bool special_case(const uint8_t* in, int32_t srcSize, int32_t outSize, int32_t* ret_slot,
@@ -848,7 +867,8 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
                                                         const uint64_t* __restrict__ dst_off,
                                                         const int32_t* __restrict__ dst_cap,
                                                         int32_t* __restrict__ ret, uint32_t nblocks,
-                                                        uint64_t* __restrict__ dbg) {
+                                                        uint64_t* __restrict__ dbg,
+                                                        const int32_t* __restrict__ dict_len) {
     const uint32_t b = blockIdx.x;
     if (b >= nblocks) return;
     const uint32_t lane = lane_id();
@@ -862,7 +882,7 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
     __shared__ __attribute__((aligned(16))) uint8_t smem[kRing + kRingPad + kSink + kSpan + kJump];
     decode_block<kStamps>(in, srcSize, out, outSize, ret + b, d, lane,
                           (lu8*)(smem + kRing + kRingPad + kSink), (lu32*)smem,
-                          (lu16*)(smem + kRing + kRingPad + kSink + kSpan));
+                          (lu16*)(smem + kRing + kRingPad + kSink + kSpan), dict_of(dict_len, b));
 }
 
 // ============================================================================
@@ -938,8 +958,6 @@ LZ4E_DEV int32_t lds_acquire(int32_t* p) {
 LZ4E_DEV void lds_release(int32_t* p, int32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// Every global store of this wave has completed (before a flag says so).
-LZ4E_DEV void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // u16 x 4 at a jump-table index (unaligned forms for the pointer runs).
 typedef uint64_t __attribute__((aligned(2))) u64a2;
@@ -1149,7 +1167,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
     const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
-    uint64_t* __restrict__ dbg) {
+    uint64_t* __restrict__ dbg, const int32_t* __restrict__ dict_len) {
     __shared__ __attribute__((aligned(16))) PipeLds S;
     const uint32_t b = blockIdx.x;
     if (b >= nblocks) return;
@@ -1176,7 +1194,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
     if (wave == 0) {
         // ---------------- parser ----------------
         Parse P;
-        P.init(in, srcSize, outSize, (lu32*)S.ring, lane);
+        P.init(in, srcSize, outSize, (lu32*)S.ring, lane, dict_of(dict_len, b));
         int32_t j = 0, lo1 = 0, lo2 = 0, hi1 = 0, hi2 = 0;
         bool hbm1 = false, hbm2 = false;
         for (;;) {
@@ -1295,12 +1313,12 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
     if (mode == kDecPipe) {
         hipLaunchKernelGGL((decompress_pipe_kernel<kStamps>), dim3(a.nblocks), dim3(kPipeWaves * kWave),
                            0, stream, a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.nblocks, dbg);
+                           a.nblocks, dbg, a.dict_len);
         return hipGetLastError();
     }
     hipLaunchKernelGGL((decompress_kernel<kStamps>), dim3(a.nblocks), dim3(kWave), 0, stream,
                        a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
-                       dbg);
+                       dbg, a.dict_len);
     return hipGetLastError();
 }
 

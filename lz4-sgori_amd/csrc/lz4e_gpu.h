@@ -24,6 +24,9 @@ struct CompressBatch {
     uint32_t* aux;  // nullable, 2 words per block
     uint32_t nblocks;
     uint32_t max_len;
+    // Dictionary mode (nullable): block i's dictionary is the dict_len[i]
+    // (<= 64 KiB) bytes right before src + src_off[i]; byU32 blocks only.
+    const uint32_t* dict_len = nullptr;
 };
 
 struct DecompressBatch {
@@ -39,6 +42,10 @@ struct DecompressBatch {
     // unknown) take the pipelined 4-wave decoder, smaller ones one wave each.
     uint32_t max_cap;
     uint32_t mode = 0;  // kDecAuto, or force kDecWave / kDecPipe (tests, A/B)
+    // Dictionary mode (nullable): block i decodes with the dict_len[i] bytes
+    // right before dst + dst_off[i] as its dictionary (extDict semantics of
+    // lz4e_decompress.c:299-302, 339-378; <= 64 KiB of it is ever read).
+    const int32_t* dict_len = nullptr;
 };
 
 enum : uint32_t { kDecAuto = 0, kDecWave = 1, kDecPipe = 2 };

@@ -279,7 +279,7 @@ int table_type_of(const struct bio_vec* bv, const struct bvec_iter* it) {
 // Descriptor block of a batch of R blocks, at `base` inside a staging
 // buffer: the inputs the kernels read, then the results they write.
 struct MetaLayout {
-    size_t src_off, src_len, ttype, dst_off, dst_cap, ret, aux, total;
+    size_t src_off, src_len, ttype, dst_off, dst_cap, dict_len, ret, aux, total;
     MetaLayout(uint32_t R, size_t base) {
         size_t o = base;
         src_off = o;  o += align16(8ull * R);
@@ -287,6 +287,7 @@ struct MetaLayout {
         ttype = o;    o += align16(1ull * R);
         dst_off = o;  o += align16(8ull * R);
         dst_cap = o;  o += align16(4ull * R);
+        dict_len = o; o += align16(4ull * R);
         ret = o;      o += align16(4ull * R);
         aux = o;      o += align16(8ull * R);
         total = o;
@@ -305,7 +306,21 @@ int lz4e_sg_table_type(const struct bio_vec* src, const struct bvec_iter* it) {
     return table_type_of(src, it);
 }
 
-int lz4e_compress_sg_batch(struct lz4e_sg_request* reqs, int n) {
+}  // extern "C"
+
+namespace {
+
+// Dictionary bytes a request compresses against: the last <= 64 KiB of its
+// dictionary, none under 8 bytes (LZ4_loadDict: dictSize < HASH_UNIT).
+uint32_t dict_used(const char* const* dicts, const int* dict_sizes, uint32_t i) {
+    if (!dicts || !dicts[i] || dict_sizes[i] < 8) return 0;
+    return (uint32_t)std::min(dict_sizes[i], 65536);
+}
+
+// lz4e_compress_sg_batch, optionally in dictionary mode (dicts != nullptr:
+// every request byU32, block i staged right after its dictionary bytes).
+int compress_sg_batch_impl(struct lz4e_sg_request* reqs, int n, const char* const* dicts,
+                           const int* dict_sizes) {
     if (n <= 0) return 0;
     g_err.clear();
     if (!gate().check()) return -1;
@@ -320,23 +335,25 @@ int lz4e_compress_sg_batch(struct lz4e_sg_request* reqs, int n) {
         if (len > LZ4E_MAX_INPUT_SIZE) continue;                                        // :245-248
         if (len >= 13 && (tt = table_type_of(reqs[i].src, reqs[i].srcIter)) == 0) continue;  // :274-277
         map.push_back(i);
-        ttype.push_back((uint8_t)tt);
+        ttype.push_back((uint8_t)(dicts ? LZ4E_TABLE_BYU32 : tt));
     }
     const uint32_t L = (uint32_t)map.size();
     if (L == 0) return 0;
 
     // One staging image, host and device alike:
-    //   [inputs | descriptors | ret/aux | frames]
+    //   [inputs (each after its dictionary bytes) | descriptors | ret/aux | frames]
     // one H2D copy of everything before ret, the compress kernel, and two
     // copy-back kernels: ret/aux, then exactly ret[i] bytes of each frame.
     std::vector<uint64_t> so(L), fo(L);
+    std::vector<uint32_t> dl(L);
     uint64_t s = 0, f = 0;
     uint32_t max_len = 0;
     for (uint32_t j = 0; j < L; ++j) {
         const lz4e_sg_request& q = reqs[map[j]];
         const uint32_t len = q.srcIter->bi_size;
-        so[j] = s;
-        s += align16(len);
+        dl[j] = dict_used(dicts, dict_sizes, map[j]);
+        so[j] = align16(s + dl[j]);
+        s = so[j] + align16(len);
         fo[j] = f;
         f += align16((uint64_t)std::min(q.dstIter->bi_size, bound_of(len)) + 64);
         max_len = std::max(max_len, len);
@@ -351,25 +368,28 @@ int lz4e_compress_sg_batch(struct lz4e_sg_request* reqs, int n) {
     for (uint32_t j = 0; j < L; ++j) {
         const lz4e_sg_request& q = reqs[map[j]];
         const uint32_t len = q.srcIter->bi_size;
+        if (dl[j]) std::memcpy(hd + so[j] - dl[j], dicts[map[j]] + dict_sizes[map[j]] - dl[j], dl[j]);
         sg_gather(q.src, *q.srcIter, hd + so[j], len);
         reinterpret_cast<uint64_t*>(hd + m.src_off)[j] = so[j];
         reinterpret_cast<uint32_t*>(hd + m.src_len)[j] = len;
         (hd + m.ttype)[j] = ttype[j];
         reinterpret_cast<uint64_t*>(hd + m.dst_off)[j] = fbase + fo[j];
         reinterpret_cast<uint32_t*>(hd + m.dst_cap)[j] = q.dstIter->bi_size;
+        reinterpret_cast<uint32_t*>(hd + m.dict_len)[j] = dl[j];
     }
     uint8_t* dd = static_cast<uint8_t*>(c.d.p);
-    const lz4e::CompressBatch a{dd,
-                                reinterpret_cast<const uint64_t*>(dd + m.src_off),
-                                reinterpret_cast<const uint32_t*>(dd + m.src_len),
-                                dd + m.ttype,
-                                dd,
-                                reinterpret_cast<const uint64_t*>(dd + m.dst_off),
-                                reinterpret_cast<const uint32_t*>(dd + m.dst_cap),
-                                reinterpret_cast<int32_t*>(dd + m.ret),
-                                reinterpret_cast<uint32_t*>(dd + m.aux),
-                                L,
-                                max_len};
+    lz4e::CompressBatch a{dd,
+                          reinterpret_cast<const uint64_t*>(dd + m.src_off),
+                          reinterpret_cast<const uint32_t*>(dd + m.src_len),
+                          dd + m.ttype,
+                          dd,
+                          reinterpret_cast<const uint64_t*>(dd + m.dst_off),
+                          reinterpret_cast<const uint32_t*>(dd + m.dst_cap),
+                          reinterpret_cast<int32_t*>(dd + m.ret),
+                          reinterpret_cast<uint32_t*>(dd + m.aux),
+                          L,
+                          max_len};
+    if (dicts) a.dict_len = reinterpret_cast<const uint32_t*>(dd + m.dict_len);
     if (!hip_ok(hipMemcpyAsync(dd, hd, m.ret, hipMemcpyHostToDevice, c.stream), "H2D") ||
         !hip_ok(lz4e::launch_compress(a, c.stream), "compress launch") ||
         !hip_ok(copy_flat(c.h_dev, dd, m.ret, m.total - m.ret, c.stream), "copy-back meta"))
@@ -396,12 +416,35 @@ int lz4e_compress_sg_batch(struct lz4e_sg_request* reqs, int n) {
     return ok;
 }
 
+}  // namespace
+
+extern "C" {
+
+int lz4e_compress_sg_batch(struct lz4e_sg_request* reqs, int n) {
+    return compress_sg_batch_impl(reqs, n, nullptr, nullptr);
+}
+
 int LZ4E_compress_default(const struct bio_vec* src, struct bio_vec* dst, struct bvec_iter* srcIter,
                           struct bvec_iter* dstIter, void* wrkmem) {
     if (wrkmem) std::memset(wrkmem, 0, LZ4E_MEM_COMPRESS);  // lz4e_compress.c:548
     if (srcIter->bi_size > LZ4E_MAX_INPUT_SIZE) return 0;
     lz4e_sg_request q{src, dst, srcIter, dstIter, 0};
     const int r = lz4e_compress_sg_batch(&q, 1);
+    return r < 0 ? 0 : q.ret;
+}
+
+int lz4e_compress_sg_batch_dict(struct lz4e_sg_request* reqs, int n, const char* const* dicts,
+                                const int* dict_sizes) {
+    return compress_sg_batch_impl(reqs, n, dicts, dict_sizes);
+}
+
+int LZ4E_compress_usingDict(const struct bio_vec* src, struct bio_vec* dst, struct bvec_iter* srcIter,
+                            struct bvec_iter* dstIter, void* wrkmem, const char* dictionary,
+                            int dictSize) {
+    if (wrkmem) std::memset(wrkmem, 0, LZ4E_MEM_COMPRESS);
+    if (srcIter->bi_size > LZ4E_MAX_INPUT_SIZE) return 0;
+    lz4e_sg_request q{src, dst, srcIter, dstIter, 0};
+    const int r = compress_sg_batch_impl(&q, 1, &dictionary, &dictSize);
     return r < 0 ? 0 : q.ret;
 }
 
@@ -416,26 +459,36 @@ uint64_t decode_staging(int csize, int cap) {
     return std::min<uint64_t>((uint64_t)cap, most);
 }
 
-int lz4e_decompress_batch(const char* const* src, const int* csize, char* const* dst, const int* cap,
-                          int* ret, int n) {
+}  // extern "C"
+
+namespace {
+
+// lz4e_decompress_batch, optionally with dictionaries: block i's output is
+// staged right after the last <= 64 KiB of its dictionary (the decoders read
+// sources before the output from there), and the whole staging image goes
+// H2D.
+int decompress_batch_impl(const char* const* src, const int* csize, char* const* dst, const int* cap,
+                          int* ret, int n, const char* const* dicts, const int* dict_sizes) {
     if (n <= 0) return 0;
     g_err.clear();
     for (int i = 0; i < n; ++i) ret[i] = -1;
     if (!gate().check()) return -1;
     const uint32_t R = (uint32_t)n;
-    // [frames | descriptors | ret | outputs]
+    // [frames | descriptors | ret | outputs (each after its dictionary bytes)]
     std::vector<uint64_t> so(R), dso(R);
+    std::vector<int32_t> dl(R, 0);
     uint64_t s = 0, d = 0;
     for (uint32_t i = 0; i < R; ++i) {
         so[i] = s;
         s += align16((uint64_t)std::max(csize[i], 0));
     }
     const size_t m_so = s, m_sl = m_so + align16(8ull * R), m_do = m_sl + align16(4ull * R),
-                 m_dc = m_do + align16(8ull * R), m_rt = m_dc + align16(4ull * R),
-                 obase = m_rt + align16(4ull * R);
+                 m_dc = m_do + align16(8ull * R), m_dl = m_dc + align16(4ull * R),
+                 m_rt = m_dl + align16(4ull * R), obase = m_rt + align16(4ull * R);
     for (uint32_t i = 0; i < R; ++i) {
-        dso[i] = obase + d;
-        d += align16(decode_staging(csize[i], cap[i]) + 64);
+        if (dicts && dicts[i] && dict_sizes[i] > 0) dl[i] = std::min(dict_sizes[i], 65536);
+        dso[i] = obase + align16(d + (uint64_t)dl[i]);
+        d = dso[i] - obase + align16(decode_staging(csize[i], cap[i]) + 64);
     }
     Lease ls;
     if (!ls.acquire()) return -1;
@@ -448,18 +501,22 @@ int lz4e_decompress_batch(const char* const* src, const int* csize, char* const*
         reinterpret_cast<int32_t*>(hd + m_sl)[i] = csize[i];
         reinterpret_cast<uint64_t*>(hd + m_do)[i] = dso[i];
         reinterpret_cast<int32_t*>(hd + m_dc)[i] = cap[i];
+        reinterpret_cast<int32_t*>(hd + m_dl)[i] = dl[i];
+        if (dl[i]) std::memcpy(hd + dso[i] - dl[i], dicts[i] + dict_sizes[i] - dl[i], (size_t)dl[i]);
     }
     uint8_t* dd = static_cast<uint8_t*>(c.d.p);
-    const lz4e::DecompressBatch a{dd,
-                                  reinterpret_cast<const uint64_t*>(dd + m_so),
-                                  reinterpret_cast<const int32_t*>(dd + m_sl),
-                                  dd,
-                                  reinterpret_cast<const uint64_t*>(dd + m_do),
-                                  reinterpret_cast<const int32_t*>(dd + m_dc),
-                                  reinterpret_cast<int32_t*>(dd + m_rt),
-                                  R,
-                                  (uint32_t)std::max(0, *std::max_element(cap, cap + n))};
-    bool ok = hip_ok(hipMemcpyAsync(dd, hd, m_rt, hipMemcpyHostToDevice, c.stream), "H2D") &&
+    lz4e::DecompressBatch a{dd,
+                            reinterpret_cast<const uint64_t*>(dd + m_so),
+                            reinterpret_cast<const int32_t*>(dd + m_sl),
+                            dd,
+                            reinterpret_cast<const uint64_t*>(dd + m_do),
+                            reinterpret_cast<const int32_t*>(dd + m_dc),
+                            reinterpret_cast<int32_t*>(dd + m_rt),
+                            R,
+                            (uint32_t)std::max(0, *std::max_element(cap, cap + n))};
+    if (dicts) a.dict_len = reinterpret_cast<const int32_t*>(dd + m_dl);
+    const uint64_t h2d = dicts ? obase + d : m_rt;  // the dictionaries live among the outputs
+    bool ok = hip_ok(hipMemcpyAsync(dd, hd, h2d, hipMemcpyHostToDevice, c.stream), "H2D") &&
               hip_ok(lz4e::launch_decompress(a, c.stream), "decompress launch") &&
               hip_ok(copy_flat(c.h_dev, dd, m_rt, 4ull * R, c.stream), "copy-back ret");
     if (ok) {
@@ -482,10 +539,35 @@ int lz4e_decompress_batch(const char* const* src, const int* csize, char* const*
     return good;
 }
 
+}  // namespace
+
+extern "C" {
+
+int lz4e_decompress_batch(const char* const* src, const int* csize, char* const* dst, const int* cap,
+                          int* ret, int n) {
+    return decompress_batch_impl(src, csize, dst, cap, ret, n, nullptr, nullptr);
+}
+
 int LZ4E_decompress_safe(const char* source, char* dest, int compressedSize, int maxDecompressedSize) {
     int r = -1;
     char* d = dest;
     if (lz4e_decompress_batch(&source, &compressedSize, &d, &maxDecompressedSize, &r, 1) < 0)
+        return r < 0 ? r : -1;
+    return r;
+}
+
+int lz4e_decompress_batch_dict(const char* const* src, const int* csize, char* const* dst,
+                               const int* cap, const char* const* dicts, const int* dict_sizes,
+                               int* ret, int n) {
+    return decompress_batch_impl(src, csize, dst, cap, ret, n, dicts, dict_sizes);
+}
+
+int LZ4E_decompress_safe_usingDict(const char* source, char* dest, int compressedSize,
+                                   int maxDecompressedSize, const char* dictStart, int dictSize) {
+    int r = -1;
+    char* d = dest;
+    if (decompress_batch_impl(&source, &compressedSize, &d, &maxDecompressedSize, &r, 1, &dictStart,
+                              &dictSize) < 0)
         return r < 0 ? r : -1;
     return r;
 }
@@ -569,6 +651,30 @@ int lz4e_decompress_batch_dev(const uint8_t* src, const uint64_t* src_off, const
                               int32_t* ret, uint32_t nblocks, uint32_t max_cap, void* stream) {
     g_err.clear();
     lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap};
+    return hip_ok(lz4e::launch_decompress(a, static_cast<hipStream_t>(stream)), "decompress launch")
+               ? 0
+               : -1;
+}
+
+int lz4e_compress_batch_dev_dict(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
+                                 const uint8_t* table_type, uint8_t* dst, const uint64_t* dst_off,
+                                 const uint32_t* dst_cap, int32_t* ret, uint32_t* aux,
+                                 uint32_t nblocks, uint32_t max_len, const uint32_t* dict_len,
+                                 void* stream) {
+    g_err.clear();
+    lz4e::CompressBatch a{src, src_off, src_len, table_type, dst, dst_off, dst_cap, ret, aux,
+                          nblocks, max_len, dict_len};
+    return hip_ok(lz4e::launch_compress(a, static_cast<hipStream_t>(stream)), "compress launch") ? 0
+                                                                                                  : -1;
+}
+
+int lz4e_decompress_batch_dev_dict(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
+                                   uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
+                                   int32_t* ret, uint32_t nblocks, uint32_t max_cap,
+                                   const int32_t* dict_len, void* stream) {
+    g_err.clear();
+    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap,
+                            0, dict_len};
     return hip_ok(lz4e::launch_decompress(a, static_cast<hipStream_t>(stream)), "decompress launch")
                ? 0
                : -1;

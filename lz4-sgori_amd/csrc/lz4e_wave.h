@@ -131,6 +131,8 @@ LZ4E_DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront
 LZ4E_DEV void lockstep() {}
 // Workgroup barrier (one wave per workgroup: orders the LDS staging).
 LZ4E_DEV void block_sync() { __syncthreads(); }
+// Every global store of this wave has completed (before a flag says so).
+LZ4E_DEV void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Moves a (possibly wave-uniform) byte offset into a VGPR.  A uniform load
 // from read-only memory would otherwise become s_load_*, which ignores the

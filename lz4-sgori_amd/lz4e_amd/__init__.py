@@ -47,6 +47,8 @@ EXPORTED_SYMBOLS = (
     "lz4e_last_error", "lz4e_gpu_available", "lz4e_compress_sg_batch",
     "lz4e_decompress_batch", "lz4e_compress_batch_dev", "lz4e_decompress_batch_dev",
     "lz4e_chunk_write_batch", "lz4e_decompress_safe_sg", "lz4e_decompress_sg_batch",
+    "LZ4E_compress_usingDict", "LZ4E_decompress_safe_usingDict", "lz4e_compress_sg_batch_dict",
+    "lz4e_decompress_batch_dict", "lz4e_compress_batch_dev_dict", "lz4e_decompress_batch_dev_dict",
 )
 
 
@@ -140,6 +142,19 @@ def lib() -> ctypes.CDLL:
     L.lz4e_decompress_safe_sg.restype = I32
     L.lz4e_decompress_sg_batch.argtypes = [P, P, P, P, P, I32]
     L.lz4e_decompress_sg_batch.restype = I32
+    L.LZ4E_compress_usingDict.argtypes = [ctypes.POINTER(BioVec), ctypes.POINTER(BioVec),
+                                          ctypes.POINTER(BvecIter), ctypes.POINTER(BvecIter), P, P, I32]
+    L.LZ4E_compress_usingDict.restype = I32
+    L.LZ4E_decompress_safe_usingDict.argtypes = [P, P, I32, I32, P, I32]
+    L.LZ4E_decompress_safe_usingDict.restype = I32
+    L.lz4e_compress_sg_batch_dict.argtypes = [ctypes.POINTER(SgRequest), I32, P, P]
+    L.lz4e_compress_sg_batch_dict.restype = I32
+    L.lz4e_decompress_batch_dict.argtypes = [P, P, P, P, P, P, P, I32]
+    L.lz4e_decompress_batch_dict.restype = I32
+    L.lz4e_compress_batch_dev_dict.argtypes = [P, P, P, P, P, P, P, P, P, U32, U32, P, P]
+    L.lz4e_compress_batch_dev_dict.restype = I32
+    L.lz4e_decompress_batch_dev_dict.argtypes = [P, P, P, P, P, P, P, U32, U32, P, P]
+    L.lz4e_decompress_batch_dev_dict.restype = I32
     _lib = L
     return L
 
@@ -273,6 +288,70 @@ def decompress_safe(source: bytes, max_decompressed_size: int,
     src = ctypes.create_string_buffer(bytes(source), max(len(source), 1))
     r = lib().LZ4E_decompress_safe(src, dst, csize, max_decompressed_size)
     return r, dst.raw[:max(r, 0)]
+
+
+def compress_using_dict(src: SgList, dst: SgList, dictionary: bytes,
+                        wrkmem: Optional[ctypes.Array] = None) -> int:
+    """LZ4E_compress_usingDict (dictionary mode, include/lz4e.h)."""
+    _require_gpu()
+    if wrkmem is None:
+        wrkmem = (ctypes.c_uint8 * LZ4E_MEM_COMPRESS)()
+    d = ctypes.create_string_buffer(bytes(dictionary), max(len(dictionary), 1))
+    return lib().LZ4E_compress_usingDict(src.bvecs, dst.bvecs, ctypes.byref(src.it),
+                                         ctypes.byref(dst.it), wrkmem, d, len(dictionary))
+
+
+def decompress_safe_using_dict(source: bytes, max_decompressed_size: int, dictionary: bytes,
+                               compressed_size: Optional[int] = None) -> Tuple[int, bytes]:
+    """LZ4E_decompress_safe_usingDict; returns (ret, dest[:max(ret, 0)])."""
+    _require_gpu()
+    csize = len(source) if compressed_size is None else compressed_size
+    dst = ctypes.create_string_buffer(max(max_decompressed_size, 0) + 1)
+    src = ctypes.create_string_buffer(bytes(source), max(len(source), 1))
+    d = ctypes.create_string_buffer(bytes(dictionary), max(len(dictionary), 1))
+    r = lib().LZ4E_decompress_safe_usingDict(src, dst, csize, max_decompressed_size, d,
+                                             len(dictionary))
+    return r, dst.raw[:max(r, 0)]
+
+
+def decompress_batch_dict(frames: Sequence[bytes], caps: Sequence[int],
+                          dicts: Sequence[bytes]) -> List[Tuple[int, bytes]]:
+    """lz4e_decompress_batch_dict over host frames; returns (ret, bytes) per frame."""
+    _require_gpu()
+    n = len(frames)
+    srcs = [ctypes.create_string_buffer(bytes(f), max(len(f), 1)) for f in frames]
+    dsts = [ctypes.create_string_buffer(max(c, 0) + 1) for c in caps]
+    dcs = [ctypes.create_string_buffer(bytes(d), max(len(d), 1)) for d in dicts]
+    sp = (ctypes.c_void_p * n)(*[ctypes.addressof(s) for s in srcs])
+    dp = (ctypes.c_void_p * n)(*[ctypes.addressof(d) for d in dsts])
+    kp = (ctypes.c_void_p * n)(*[ctypes.addressof(d) for d in dcs])
+    ks = (ctypes.c_int * n)(*[len(d) for d in dicts])
+    cs = (ctypes.c_int * n)(*[len(f) for f in frames])
+    cp = (ctypes.c_int * n)(*caps)
+    rt = (ctypes.c_int * n)()
+    if lib().lz4e_decompress_batch_dict(sp, cs, dp, cp, kp, ks, rt, n) < 0:
+        raise GpuUnavailable(last_error())
+    return [(rt[i], dsts[i].raw[:max(rt[i], 0)]) for i in range(n)]
+
+
+def compress_sg_batch_dict(pairs: Sequence[Tuple[SgList, SgList]],
+                           dicts: Sequence[bytes]) -> List[int]:
+    """lz4e_compress_sg_batch_dict; returns each ret."""
+    _require_gpu()
+    n = len(pairs)
+    reqs = (SgRequest * n)()
+    for i, (s, d) in enumerate(pairs):
+        reqs[i].src = s.bvecs
+        reqs[i].dst = d.bvecs
+        reqs[i].srcIter = ctypes.pointer(s.it)
+        reqs[i].dstIter = ctypes.pointer(d.it)
+    dcs = [ctypes.create_string_buffer(bytes(d), max(len(d), 1)) for d in dicts]
+    kp = (ctypes.c_void_p * n)(*[ctypes.addressof(d) for d in dcs])
+    ks = (ctypes.c_int * n)(*[len(d) for d in dicts])
+    r = lib().lz4e_compress_sg_batch_dict(reqs, n, kp, ks)
+    if r < 0:
+        raise GpuUnavailable(last_error())
+    return [reqs[i].ret for i in range(n)]
 
 
 def compress_sg_batch(pairs: Sequence[Tuple[SgList, SgList]]) -> List[int]:

@@ -311,7 +311,33 @@ int oracle_compress_linear(const uint8_t *in, uint32_t n, int table_type,
 	struct lin_dst d = { out };
 
 	return compress_core_linear(&s, n, table_type, &d, cap, final_src,
-				    last_run);
+				    last_run, 0);
+}
+
+/* Dictionary mode (the reference's stubbed dict path, lz4e_compress.c:250-266,
+ * 315-324; LZ4E extension, parity unpinned): the block compressed against the
+ * last <= 64 KiB of dict (ignored under 8 bytes, LZ4_loadDict), byU32. */
+int oracle_compress_dict(const uint8_t *in, uint32_t n, const uint8_t *dict,
+			 uint32_t dict_size, uint8_t *out, uint32_t cap)
+{
+	uint32_t D = dict_size > 65536 ? 65536 : dict_size;
+	uint8_t *img;
+	struct lin_src s;
+	struct lin_dst d = { out };
+	int r;
+
+	if (D < 8)
+		D = 0;
+	img = malloc((size_t)D + n + 16);
+	if (!img)
+		return 0;
+	memcpy(img, dict + dict_size - D, D);
+	memcpy(img + D, in, n);
+	s.p = img;
+	r = compress_core_linear(&s, n, LZ4E_TABLE_BYU32,
+				 &d, cap, NULL, NULL, D);
+	free(img);
+	return r;
 }
 
 /* Kernel bvec_iter_advance semantics (warn + clamp past the end). */
@@ -355,7 +381,7 @@ int oracle_compress_sg(const struct bio_vec *src, struct bio_vec *dst,
 	}
 	sg_build(&sl, src, srcIter);
 	sg_build(&dl, dst, dstIter);
-	ret = compress_core_sg(&sl, n, tt, &dl, cap, &final_src, &last_run);
+	ret = compress_core_sg(&sl, n, tt, &dl, cap, &final_src, &last_run, 0);
 	free(sl.base);
 	free(dl.base);
 	if (ret > 0) {
@@ -377,8 +403,28 @@ int oracle_compress_sg(const struct bio_vec *src, struct bio_vec *dst,
 int oracle_decompress_safe(const char *src, char *dst, int srcSize,
 			   int outSize)
 {
+	return oracle_decompress_dict(src, dst, srcSize, outSize, NULL, 0);
+}
+
+/* Output byte at position x >= -D: the block, or before it the dictionary's
+ * last bytes (extDict, lz4e_decompress.c:339-378). */
+static inline uint8_t o_out(const uint8_t *d, const uint8_t *dict_end,
+			    int64_t x)
+{
+	return x >= 0 ? d[x] : dict_end[x];
+}
+
+/* The reference decoder with a dictionary (usingExtDict, lowPrefix = dst,
+ * dictStart/dictSize): checkOffset when dictSize < 64 KiB (:93), the
+ * shortcut only for sources inside the block (:170-172), sources before the
+ * block read from the dictionary's end (:339-378). */
+int oracle_decompress_dict(const char *src, char *dst, int srcSize,
+			   int outSize, const char *dict, int dictSize)
+{
 	const uint8_t *s = (const uint8_t *)src;
 	uint8_t *d = (uint8_t *)dst;
+	const uint8_t *dict_end = dict ? (const uint8_t *)dict + dictSize : NULL;
+	const int64_t dsz = dict && dictSize > 0 ? dictSize : 0;
 	const int64_t iend = srcSize, oend = outSize;
 	const int64_t shortiend = iend - 14 - 2; /* :100-101 */
 	const int64_t shortoend = oend - 14 - 18; /* :102-103 */
@@ -447,7 +493,7 @@ int oracle_decompress_safe(const char *src, char *dst, int srcSize,
 		length = token & 15;
 
 copy_match:
-		if (match < 0) /* :299-302 */
+		if (dsz < 65536 && match + dsz < 0) /* :299-302 */
 			goto err;
 		if (length == 15) { /* :316-334 */
 			unsigned b;
@@ -467,7 +513,7 @@ copy_match:
 			memset(d + op, 0, (size_t)length);
 		else
 			for (t = 0; t < length; t++)
-				d[op + t] = d[match + t];
+				d[op + t] = o_out(d, dict_end, match + t);
 		op = cpy;
 	}
 	return (int)op;

@@ -41,6 +41,14 @@ int oracle_compress_sg(const struct bio_vec *src, struct bio_vec *dst,
 		       struct bvec_iter *srcIter, struct bvec_iter *dstIter,
 		       void *wrkmem);
 
+/* Dictionary mode (LZ4E extension of the stubbed dict path, parity
+ * unpinned): compress against the last <= 64 KiB of dict, decode with a
+ * dictionary (extDict branches of lz4e_decompress.c:299-302, 339-378). */
+int oracle_compress_dict(const uint8_t *in, uint32_t n, const uint8_t *dict,
+			 uint32_t dict_size, uint8_t *out, uint32_t cap);
+int oracle_decompress_dict(const char *src, char *dst, int srcSize,
+			   int outSize, const char *dict, int dictSize);
+
 /* Safe full-block decoder (lz4e/lz4e_decompress.c:62-469). */
 int oracle_decompress_safe(const char *src, char *dst, int srcSize,
 			   int outSize);

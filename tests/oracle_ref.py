@@ -45,6 +45,10 @@ def load():
     L.oracle_compress_sg_batch.restype = None
     L.oracle_decompress_batch.argtypes = [P, P, P, P, P, P, P, U32, I32]
     L.oracle_decompress_batch.restype = None
+    L.oracle_compress_dict.argtypes = [P, U32, P, U32, P, U32]
+    L.oracle_compress_dict.restype = I32
+    L.oracle_decompress_dict.argtypes = [P, P, I32, I32, P, I32]
+    L.oracle_decompress_dict.restype = I32
     _lib = L
     return L
 
@@ -68,6 +72,29 @@ def decompress(frame: bytes, cap: int, csize=None):
     out = ctypes.create_string_buffer(max(cap, 0) + 64)
     src = ctypes.create_string_buffer(bytes(frame), max(len(frame), 1))
     r = L.oracle_decompress_safe(src, out, csize, cap)
+    return r, out.raw[:max(r, 0)]
+
+
+def compress_dict(data: bytes, dictionary: bytes, cap=None):
+    """Dictionary mode (LZ4E extension, parity unpinned) -> (ret, frame)."""
+    L = load()
+    n = len(data)
+    cap = n + n // 255 + 16 if cap is None else cap
+    out = ctypes.create_string_buffer(max(cap, 1) + 64)
+    src = ctypes.create_string_buffer(bytes(data), max(n, 1))
+    dct = ctypes.create_string_buffer(bytes(dictionary), max(len(dictionary), 1))
+    r = L.oracle_compress_dict(src, n, dct, len(dictionary), out, cap)
+    return r, out.raw[:max(r, 0)]
+
+
+def decompress_dict(frame: bytes, cap: int, dictionary: bytes, csize=None):
+    """-> (ret, bytes[:max(ret,0)]) decoding with a dictionary."""
+    L = load()
+    csize = len(frame) if csize is None else csize
+    out = ctypes.create_string_buffer(max(cap, 0) + 64)
+    src = ctypes.create_string_buffer(bytes(frame), max(len(frame), 1))
+    dct = ctypes.create_string_buffer(bytes(dictionary), max(len(dictionary), 1))
+    r = L.oracle_decompress_dict(src, out, csize, cap, dct, len(dictionary))
     return r, out.raw[:max(r, 0)]
 
 

@@ -73,3 +73,82 @@ def test_emulated_kernel_sanitized(emu_exe, tmp_path, kind, n, cls):
     assert int(r) == er
     assert frame.read_bytes() == ef
     assert (int(fs), int(lr)) == (efs, elr)
+
+
+DICT_CASES = [("text", 4096, 4096), ("records", 16384, 65536), ("ints", 8192, 100000),
+              ("text", 20000, 9), ("text", 20000, 5), ("random", 5000, 3000), ("text", 12, 4096)]
+
+
+@pytest.mark.parametrize("kind,n,dsize", DICT_CASES, ids=[f"{k}-{n}-d{d}" for k, n, d in DICT_CASES])
+def test_emulated_kernel_dictionary_sanitized(emu_exe, tmp_path, kind, n, dsize):
+    """Dictionary mode (LZ4E extension, parity unpinned) through the kernel
+    source: the dictionary preload, a parse starting after the dictionary and
+    candidates inside it, under ASan + UBSan; frames equal the oracle's and
+    decode back with the dictionary."""
+    data = _block(kind, n + dsize, 7 + n).tobytes()
+    dic, blkb = data[:dsize], data[dsize:]
+    blk, frame, dct = tmp_path / "blk.bin", tmp_path / "frame.bin", tmp_path / "dict.bin"
+    blk.write_bytes(blkb)
+    dct.write_bytes(dic)
+    out = subprocess.run([emu_exe, str(blk), str(BYU32), str(frame), str(dct)], capture_output=True,
+                         text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "ERROR: AddressSanitizer" not in out.stderr and "runtime error" not in out.stderr
+    r = int(out.stdout.split()[1])
+    er, ef = oracle_ref.compress_dict(blkb, dic)
+    assert r == er
+    assert frame.read_bytes() == ef
+    assert oracle_ref.decompress_dict(ef, n, dic) == (n, blkb)
+
+
+# ---------------------------------------------------------------------------
+# the one-wave decoder's source on the CPU (emu_main -d), ASan + UBSan: the
+# output buffer is exactly [dictionary | capacity], so a read before the
+# dictionary or a write past the capacity is caught
+# ---------------------------------------------------------------------------
+
+def _emu_decode(exe, tmp_path, frame, cap, dic=b""):
+    f, o, d = tmp_path / "f.bin", tmp_path / "o.bin", tmp_path / "d.bin"
+    f.write_bytes(frame)
+    d.write_bytes(dic)
+    if o.exists():
+        o.unlink()
+    out = subprocess.run([exe, "-d", str(f), str(cap), str(o), str(d)], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "ERROR: AddressSanitizer" not in out.stderr and "runtime error" not in out.stderr
+    r = int(out.stdout.split()[1])
+    return r, (o.read_bytes() if r > 0 else b"")
+
+
+DEC_CASES = [(k, m) for k in ("text", "records", "runs", "small_alpha") for m in range(5)]
+
+
+@pytest.mark.parametrize("kind,mode", DEC_CASES, ids=[f"{k}-{m}" for k, m in DEC_CASES])
+def test_emulated_decoder_sanitized(emu_exe, tmp_path, kind, mode):
+    """Valid frames (mode 0), truncations (1), bit flips (2), short capacity
+    (3) and a dictionary (4; with a shortened dictionary on odd seeds): the
+    decoder's values, error codes and bytes equal the oracle's."""
+    rng = np.random.default_rng(100 + mode)
+    for rep in range(3):
+        n = int(rng.integers(13, 20000))
+        data = _block(kind, n + 9000, 3 + rep + n).tobytes()
+        dic, blk = (data[:9000], data[9000:]) if mode == 4 else (b"", data[:n])
+        f = oracle_ref.compress_dict(blk, dic)[1] if mode == 4 else oracle_ref.compress(blk, BYU16)[1]
+        cap = len(blk)
+        if mode == 1:
+            f = f[:int(rng.integers(1, len(f)))]
+        elif mode == 2:
+            fb = bytearray(f)
+            for _ in range(3):
+                fb[int(rng.integers(0, len(fb)))] ^= 1 << int(rng.integers(0, 8))
+            f = bytes(fb)
+        elif mode == 3:
+            cap = max(0, cap - int(rng.integers(1, 40)))
+        elif mode == 4 and rep % 2:
+            dic = dic[int(rng.integers(1, len(dic) - 8)):]
+        want = oracle_ref.decompress_dict(f, cap, dic)
+        got = _emu_decode(emu_exe, tmp_path, f, cap, dic)
+        assert got[0] == want[0], (rep, got[0], want[0])
+        if want[0] >= 0:
+            assert got[1] == want[1], rep

@@ -670,3 +670,156 @@ def test_decompress_pipelined_vs_wave_decoder(gpu, kind):
         assert r_wg[i] == er == r_wv[i], (i, r_wg[i], er, r_wv[i])
         if er >= 0:
             assert o_wg[i] == eb == o_wv[i], i
+
+
+# ---------------------------------------------------------------------------
+# dictionary mode: LZ4E extension of the reference's
+# stubbed dict path, checked against the oracle's restatement (parity
+# unpinned: the reference never runs this path)
+# ---------------------------------------------------------------------------
+
+DICT_SIZES = [0, 5, 8, 100, 4096, 65536, 100000]
+
+
+def test_dict_compress_via_entry_point(gpu):
+    """LZ4E_compress_usingDict through bio_vec layouts (4 KiB and 512 B
+    segments, mid-segment starts) equals the oracle; the frame decodes with
+    the dictionary."""
+    rng = np.random.default_rng(21)
+    pool = _corpus("mixed", 1 << 21, 21).tobytes()
+    for i in range(28):
+        dsize = DICT_SIZES[i % len(DICT_SIZES)]
+        n = int(rng.choice([0, 12, 13, 1000, 4096, 30000, 65536]))
+        s0 = int(rng.integers(dsize, len(pool) - n))
+        dic, blk = pool[s0 - dsize:s0], pool[s0:s0 + n]
+        seg = [4096, 512][i % 2]
+        segs = [min(seg, n - j) for j in range(0, n, seg)] or [16]
+        src = make_sg(blk, segs, shuffle_seed=i)
+        cap = compress_bound(n)
+        dst = make_sg(b"", [4096] * (-(-cap // 4096) or 1), capacity=cap)
+        r = gpu.compress_using_dict(src, dst, dic)
+        er, ef = oracle_ref.compress_dict(blk, dic)
+        assert r == er, (i, n, dsize)
+        got = dst.read_prefix(r)
+        assert got == ef, (i, n, dsize)
+        assert oracle_ref.decompress_dict(got, n, dic) == (n, blk)
+
+
+def test_dict_compress_sg_batch(gpu):
+    rng = np.random.default_rng(22)
+    pool = _corpus("text", 1 << 20, 22).tobytes()
+    pairs, dicts, want = [], [], []
+    for i in range(20):
+        dsize = DICT_SIZES[i % len(DICT_SIZES)]
+        n = int(rng.integers(13, 65537))
+        s0 = int(rng.integers(dsize, len(pool) - n))
+        dic, blk = pool[s0 - dsize:s0], pool[s0:s0 + n]
+        src = make_sg(blk, [min(4096, n - j) for j in range(0, n, 4096)])
+        cap = compress_bound(n)
+        dst = make_sg(b"", [4096] * (-(-cap // 4096)), capacity=cap)
+        pairs.append((src, dst))
+        dicts.append(dic)
+        want.append(oracle_ref.compress_dict(blk, dic))
+    rets = gpu.compress_sg_batch_dict(pairs, dicts)
+    for i, (er, ef) in enumerate(want):
+        assert rets[i] == er
+        assert pairs[i][1].read_prefix(rets[i]) == ef
+
+
+@pytest.mark.parametrize("big", [False, True], ids=["wave", "pipe"])
+def test_dict_decompress_values_and_codes(gpu, big):
+    """LZ4E_decompress_safe_usingDict / lz4e_decompress_batch_dict on valid
+    frames, short dictionaries, truncations and bit flips: values, error
+    codes and bytes equal the oracle's restatement of the extDict branches
+    (lz4e_decompress.c:299-302, 339-378).  Batches of small blocks decode on
+    the one-wave decoder, batches with 64 KiB blocks on the pipelined one."""
+    rng = np.random.default_rng(23 + big)
+    pool = _corpus("mixed", 1 << 21, 23).tobytes()
+    frames, caps, dicts, want = [], [], [], []
+    for i in range(48):
+        dsize = DICT_SIZES[i % len(DICT_SIZES)]
+        n = int(rng.choice([65536, 40000])) if big and i % 3 == 0 else int(rng.integers(13, 12000))
+        s0 = int(rng.integers(dsize, len(pool) - n))
+        dic, blk = pool[s0 - dsize:s0], pool[s0:s0 + n]
+        f = oracle_ref.compress_dict(blk, dic)[1]
+        mode = i % 5
+        cap = n
+        if mode == 1 and len(dic) > 20:
+            dic = dic[int(rng.integers(1, len(dic) - 8)):]  # a shorter dictionary
+        elif mode == 2 and len(f) > 2:
+            f = f[:int(rng.integers(1, len(f)))]
+        elif mode == 3 and len(f) > 0:
+            fb = bytearray(f)
+            for _ in range(3):
+                fb[int(rng.integers(0, len(fb)))] ^= 1 << int(rng.integers(0, 8))
+            f = bytes(fb)
+        elif mode == 4:
+            cap = max(0, n - int(rng.integers(1, 64)))
+        frames.append(f)
+        caps.append(cap)
+        dicts.append(dic)
+        want.append(oracle_ref.decompress_dict(f, cap, dic))
+    got = gpu.decompress_batch_dict(frames, caps, dicts)
+    for i, (er, eb) in enumerate(want):
+        assert got[i][0] == er, (i, got[i][0], er)
+        if er >= 0:
+            assert got[i][1] == eb, i
+    # the single-call entry point on a few of them
+    for i in range(0, 48, 7):
+        assert gpu.decompress_safe_using_dict(frames[i], caps[i], dicts[i]) == want[i]
+
+
+def test_dict_streams_device_resident(gpu):
+    """Streams of 64 KiB blocks where block k's dictionary is block k-1
+    (dict_len bytes right before the block in HBM): one compress launch over
+    every block of every stream (blocks are independent given their
+    dictionaries), frames equal the oracle's; then decode block index by block
+    index across the streams, each block's dictionary being the previous
+    block's decoded output in place -- the stream round trips."""
+    import torch
+    amd = gpu
+    S, K, bs = 6, 5, 65536
+    dev = torch.device("cuda")
+    host = _corpus("mixed", S * K * bs, 24)
+    src = torch.from_numpy(host).to(dev)
+    n = S * K
+    offs = np.arange(n, dtype=np.int64) * bs                  # stream s block k at (s*K + k) * bs
+    dlen = np.array([min(k * bs, 65536) for s in range(S) for k in range(K)], np.int64)
+    cap = bs + bs // 255 + 16
+    slot = (cap + 64 + 15) // 16 * 16
+    doffs = np.arange(n, dtype=np.int64) * slot
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).to(dev)
+    dst = torch.zeros(n * slot, dtype=torch.uint8, device=dev)
+    ret = torch.zeros(n, dtype=torch.int32, device=dev)
+    L = amd.lib()
+    ptr = lambda x: x.data_ptr()
+    d_off, d_len, d_tt = t(offs, np.int64), t(np.full(n, bs), np.int32), t(np.full(n, BYU32), np.uint8)
+    d_doff, d_cap, d_dl = t(doffs, np.int64), t(np.full(n, cap), np.int32), t(dlen, np.int32)
+    assert L.lz4e_compress_batch_dev_dict(ptr(src), ptr(d_off), ptr(d_len), ptr(d_tt), ptr(dst),
+                                          ptr(d_doff), ptr(d_cap), ptr(ret), None, n, bs,
+                                          ptr(d_dl), None) == 0
+    torch.cuda.synchronize()
+    r = ret.cpu().numpy()
+    d = dst.cpu().numpy()
+    for i in range(n):
+        k = i % K
+        blk = host[i * bs:(i + 1) * bs].tobytes()
+        dic = host[i * bs - int(dlen[i]):i * bs].tobytes() if k else b""
+        er, ef = oracle_ref.compress_dict(blk, dic)
+        assert r[i] == er and d[doffs[i]:doffs[i] + r[i]].tobytes() == ef, i
+    # decode: launch k decodes block k of every stream into the stream's
+    # contiguous output, after block k-1 (its dictionary)
+    out = torch.zeros(n * bs + 64, dtype=torch.uint8, device=dev)
+    dret = torch.full((n,), -9, dtype=torch.int32, device=dev)
+    for k in range(K):
+        idx = np.array([s * K + k for s in range(S)])
+        a_soff, a_slen = t(doffs[idx], np.int64), t(r[idx], np.int32)
+        a_doff, a_cap, a_dl = t(offs[idx], np.int64), t(np.full(S, bs), np.int32), t(dlen[idx], np.int32)
+        rr = torch.zeros(S, dtype=torch.int32, device=dev)
+        assert L.lz4e_decompress_batch_dev_dict(ptr(dst), ptr(a_soff), ptr(a_slen), ptr(out),
+                                                ptr(a_doff), ptr(a_cap), ptr(rr), S, bs,
+                                                ptr(a_dl), None) == 0
+        dret[torch.from_numpy(idx).to(dev)] = rr
+    torch.cuda.synchronize()
+    assert (dret.cpu().numpy() == bs).all()
+    assert np.array_equal(out[:n * bs].cpu().numpy(), host)

@@ -219,3 +219,46 @@ def test_sg_batch_equals_linear_batch():
                                    nb, 4)
         assert (r1 == r2).all() and (r1 > 0).all()
         assert np.array_equal(o1, o2)
+
+
+# ---------------------------------------------------------------------------
+# dictionary mode (LZ4E extension of the reference's
+# stubbed dict path -- no reference run pins these frames: parity unpinned)
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("n", [0, 12, 13, 4096, 65536])
+@pytest.mark.parametrize("dsize", [0, 7, 8, 1000, 65536, 90000])
+def test_dict_round_trip(n, dsize):
+    data = corpus.silesia_proxy(n + dsize + 65536, 31).tobytes()
+    dic, blk = data[:dsize], data[dsize:dsize + n]
+    r, f = oracle_ref.compress_dict(blk, dic)
+    assert r > 0
+    assert oracle_ref.decompress_dict(f, n, dic) == (n, blk)
+    # the decoder reads at most the last 64 KiB of the dictionary
+    assert oracle_ref.decompress_dict(f, n, dic[-65536:]) == (n, blk)
+    if dsize < 8:
+        # under 8 bytes the dictionary is ignored (LZ4_loadDict): byU32 noDict frame
+        assert f == oracle_ref.compress(blk, BYU32)[1]
+
+
+def test_dict_helps_and_is_needed():
+    data = corpus.text_proxy(3 * 65536, 5).tobytes()
+    dic, blk = data[:65536], data[65536:131072]
+    r0 = oracle_ref.compress(blk, BYU32)[0]
+    r, f = oracle_ref.compress_dict(blk, dic)
+    assert r < r0  # the dictionary's history shortens the frame
+    # without (or with too short) a dictionary the frame references before
+    # the output: the offset check of lz4e_decompress.c:299-302 fails it
+    assert oracle_ref.decompress(f, len(blk))[0] < 0
+    assert oracle_ref.decompress_dict(f, len(blk), dic[-16:])[0] < 0
+
+
+def test_dict_decoder_offset_check():
+    """extDict semantics: a match may reach dictSize bytes before the output;
+    one byte further fails at the offset's position (checkOffset, :93, :299)
+    unless the dictionary is 64 KiB or more (no check)."""
+    frame = bytes([0x00, 0x05, 0x00, 0x50]) + b"abcde"  # match of 4 at offset 5, then 5 literals
+    assert oracle_ref.decompress_dict(frame, 100, b"XYZUV") == (9, b"XYZU" + b"abcde")
+    assert oracle_ref.decompress_dict(frame, 100, b"YZUV")[0] == -4
+    big = bytes(range(256)) * 256  # 64 KiB
+    assert oracle_ref.decompress_dict(frame, 100, big)[0] == 9

@@ -46,3 +46,14 @@ extern "C" int emu_compress_batch(const uint8_t* src, const uint64_t* src_off, c
                           nblocks, max_len};
     return lz4e::launch_compress(a, nullptr) == hipSuccess ? 0 : -1;
 }
+
+// Dictionary mode: block i's dictionary is the dict_len[i] bytes before it.
+extern "C" int emu_compress_batch_dict(const uint8_t* src, const uint64_t* src_off,
+                                       const uint32_t* src_len, const uint8_t* table_type,
+                                       uint8_t* dst, const uint64_t* dst_off, const uint32_t* dst_cap,
+                                       int32_t* ret, uint32_t* aux, uint32_t nblocks, uint32_t max_len,
+                                       const uint32_t* dict_len) {
+    lz4e::CompressBatch a{src, src_off, src_len, table_type, dst, dst_off, dst_cap, ret, aux,
+                          nblocks, max_len, dict_len};
+    return lz4e::launch_compress(a, nullptr) == hipSuccess ? 0 : -1;
+}

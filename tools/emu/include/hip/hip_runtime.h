@@ -11,7 +11,7 @@
 #define __host__
 #define __global__
 #define __forceinline__ inline
-#define __launch_bounds__(x)
+#define __launch_bounds__(...)
 #define __shared__
 
 struct uint4 {
@@ -29,7 +29,27 @@ inline hipError_t hipGetLastError() { return hipSuccess; }
 inline hipError_t hipMalloc(void**, size_t) { return hipErrorOutOfMemory; }
 inline hipError_t hipFree(void*) { return hipSuccess; }
 
+// LDS atomic max (the dictionary preload): a CAS loop on host memory.
+inline uint32_t atomicMax(uint32_t* p, uint32_t v) {
+    uint32_t cur = __atomic_load_n(p, __ATOMIC_RELAXED);
+    while (cur < v && !__atomic_compare_exchange_n(p, &cur, v, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+    }
+    return cur;
+}
+
+// Only so that the pipelined decoder compiles (it is never run here: the
+// emulator runs one 64-lane wave per block).
+#define __HIP_MEMORY_SCOPE_WORKGROUP 0
+#define __hip_atomic_load(p, order, scope) __atomic_load_n(p, order)
+#define __hip_atomic_store(p, v, order, scope) __atomic_store_n(p, v, order)
+#define __builtin_amdgcn_s_sleep(x) ((void)0)
+inline void __syncthreads() {}
+inline bool __syncthreads_or(int v) { return v != 0; }
+inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
+    return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
+}
 extern dim3 blockIdx;
+extern thread_local dim3 threadIdx;
 void emu_launch(uint32_t nblocks, std::function<void()> lane_body);
 #define hipLaunchKernelGGL(k, grid, block, lds, stream, ...) \
     emu_launch((grid).x, [&]() { k(__VA_ARGS__); })

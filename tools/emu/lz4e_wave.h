@@ -107,9 +107,12 @@ LZ4E_DEV uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (r & 3)));
 }
 LZ4E_DEV uint64_t clock64() { return 0; }
-LZ4E_DEV void wave_fence() {}
+// The decoder orders a phase's LDS / global accesses after the previous
+// phase's with wave_fence (lockstep on the GPU): a barrier here.
+LZ4E_DEV void wave_fence() { g_wave->bar.arrive_and_wait(); }
 LZ4E_DEV void lockstep() { g_wave->bar.arrive_and_wait(); }
 LZ4E_DEV void block_sync() { g_wave->bar.arrive_and_wait(); }
+LZ4E_DEV void stores_done() {}
 LZ4E_DEV uint32_t vaddr(uint32_t q) { return q; }
 
 typedef const uint32_t gcu32;
