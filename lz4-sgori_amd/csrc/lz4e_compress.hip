@@ -409,6 +409,20 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
         // raising the priority of the waves furthest behind shortens it
         // (silesia64k compress -9 %); 4 KiB blocks finish in a few windows.
         uint32_t prio_q = n > 16384 ? 4 : 5;
+        // Put pattern the clash fixpoint starts from for the lanes ahead of a
+        // chain: every lane, or (periodic data: ints, records) the previous
+        // window's final puts, whichever predicted the last window better.
+        uint64_t guess = ~0ull, pprev = ~0ull;
+        // The next window's bytes, loaded as soon as the walk knows where it
+        // starts (nB) so that the loads overlap the emit and the commit.
+        uint32_t nB = ~0u, ndm1 = 0, ndv[kFwdW];
+        auto preload = [&](uint32_t Bn) {
+            if (Bn == nB) return;
+            nB = Bn;
+            ndm1 = img.wld(Bn + lane - 4);
+#pragma unroll
+            for (uint32_t i = 0; i < kFwdW; ++i) ndv[i] = img.wld(Bn + lane + 4 * i);
+        };
         for (;;) {
             // ================= window setup =================================
             if (prio_q != 5) {
@@ -422,10 +436,16 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             const uint32_t B = rmode ? e - 2 : e;
             const uint32_t p = B + lane;
             const bool valid = p <= mflimit;  // every put / lookup is at <= mflimit
-            const uint32_t dm1 = img.wld(p - 4);
-            uint32_t dv[kFwdW];  // bytes p .. p + kFwd - 1
+            uint32_t dm1, dv[kFwdW];  // bytes p - 4 .. p - 1, p .. p + kFwd - 1
+            if (B == nB) {
+                dm1 = ndm1;
 #pragma unroll
-            for (uint32_t i = 0; i < kFwdW; ++i) dv[i] = img.wld(p + 4 * i);
+                for (uint32_t i = 0; i < kFwdW; ++i) dv[i] = ndv[i];
+            } else {
+                dm1 = img.wld(p - 4);
+#pragma unroll
+                for (uint32_t i = 0; i < kFwdW; ++i) dv[i] = img.wld(p + 4 * i);
+            }
             const uint32_t d0 = dv[0];
             const uint32_t h = hash_val<TT>(((uint64_t)dv[1] << 32) | d0);
             uint32_t c0 = 0, rb = p;
@@ -556,7 +576,8 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                             fe = fe0;
                             jv = jv0;
                         }
-                        uint64_t Pg = put | (1ull << (ks - 2)) | lane_range(ks, 63);
+                        uint64_t Pg = put | (1ull << (ks - 2)) | (1ull << ks) |
+                                      (guess & lane_range(ks, 63));
                         constexpr uint32_t kMaxPass = 6;
                         for (uint32_t pass = 0;; ++pass) {
                             if (kStamps) st.cnt[2]++;
@@ -624,6 +645,16 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                             const bool bad = ((U >> lane) & 1) && cg != cn &&
                                              (cg == 0 || cn == 0 ||
                                               __builtin_clzll(cg) != __builtin_clzll(cn));
+#ifdef LZ4E_EMU_TRACE
+                            {
+                                const uint64_t bm = ballot(bad);
+                                if (lane == 0)
+                                    printf("W B=%u ks=%u pass=%u k=%u Pg=%016llx Pn=%016llx U=%016llx bad=%016llx g=%016llx clash=%016llx\n",
+                                           B, ks, pass, k, (unsigned long long)Pg, (unsigned long long)Pn,
+                                           (unsigned long long)U, (unsigned long long)bm,
+                                           (unsigned long long)guess, (unsigned long long)clash);
+                            }
+#endif
                             if (!ballot(bad)) break;  // fixpoint
                             if (pass + 1 == kMaxPass) {          // give up: exact walk
                                 nev = 0;
@@ -823,6 +854,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
             if (kStamps) st.lap(kPhStripe);
 
             // ================= commit the window's puts =====================
+            if (!generic) preload(rmode ? e - 2 : e);
             if (valid) {
                 const uint64_t pg = same & put;
                 bool writer;
@@ -838,6 +870,12 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                     v = c0;
                 }
                 if (writer) T.put(h, v);
+            }
+            {
+                const uint64_t R = ~7ull;
+                const uint32_t mp = popc64((put ^ pprev) & R), mo = popc64(~put & R);
+                guess = mp < mo ? put : ~0ull;
+                pprev = put;
             }
             if (kStamps) st.lap(kPhRematch);
             if (!generic) continue;
