@@ -979,14 +979,19 @@ LZ4E_DEV int32_t wave_min_i32(int32_t v) {
 // store completion; internal rounds, batches with internal pointers.
 enum { kStParse, kStPWait, kStWork, kStRec, kStFar, kStPrev, kStStore, kStBatches, kStLoads,
        kStRounds, kStGather, kStSpass, kStVm, kStNRounds, kStNInt, kStUnused, kStSlots };
+// The accumulators live in LDS (a row per wave), so that the stamped build
+// has the register allocation of the real one.
 struct PipeStamps {
-    uint64_t acc[kStSlots] = {};
+    uint64_t* acc = nullptr;  // LDS row of this wave (stamped build)
     uint64_t t = 0;
     LZ4E_DEV void lap(bool on, int k) {
         if (!on) return;
         const uint64_t now = clock64();
-        acc[k] += now - t;
+        if (lane_id() == 0) acc[k] += now - t;
         t = now;
+    }
+    LZ4E_DEV void bump(bool on, int k) {
+        if (on && lane_id() == 0) acc[k]++;
     }
 };
 
@@ -1051,6 +1056,7 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
     const bool ptrs = valid && b.off != 0 && nf < b.M;
     if (ptrs) {
         lu16* e = jt + (ms - a0);
+#pragma clang loop unroll(disable) vectorize(disable)
         for (int32_t t = nf; t < b.M; ++t) {
             const int32_t y = ss + t;
             e[t] = (uint16_t)(y < lo ? (int32_t)kCross + (y - F) : y - a0);
@@ -1060,6 +1066,7 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
     const bool has_int = ptrs && ss + b.M > lo;
     // rounds and gather start at the first pointer byte
     const int32_t i0 = (int32_t)uni((uint32_t)wave_min_i32(ptrs ? ms + nf - a0 : s1));
+    st.lap(kStamps, kStUnused);
     // the loaded bytes into the span
     if (valid && b.L > 0) {
         if (lfast) put16(span + (b.op - a0), lv, (uint32_t)b.L, sink);
@@ -1076,36 +1083,57 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
         for (int32_t t = 0; t < b.M; ++t) span[ms - a0 + t] = 0;
     wave_fence();
     st.lap(kStamps, kStLoads);
-    // internal pointers: pointer jumping until each byte is final or cross
-    // (four span bytes per lane per step: their reads are independent)
+    // internal pointers: pointer jumping until each byte is final or cross.
+    // Lane l owns the 8 span bytes / jump entries at g = b0 + 8l (+ 512k):
+    // one 16-byte entry read and one 8-byte span read per group, the 8
+    // dependent entry reads and byte reads independent of each other, and
+    // one write back of each (positions outside [i0, s1) keep their values).
+    const int32_t b0 = i0 & ~7;
+    auto entry = [&](const u32x4& jv, int q, int32_t g) -> uint32_t {
+        const uint32_t e = (jv[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+        return (g + q >= i0 && g + q < s1) ? e : kFinal;
+    };
     if (ballot(has_int)) {
-        if (kStamps) st.acc[kStNInt]++;
+        st.bump(kStamps, kStNInt);
         for (;;) {
-            if (kStamps) st.acc[kStNRounds]++;
+            st.bump(kStamps, kStNRounds);
             bool more = false;
-            for (int32_t g = i0 + (int32_t)lane; g < s1; g += 4 * kWave) {
-                uint32_t v[4], w[4], sv[4];
+            for (int32_t g = b0 + 8 * (int32_t)lane; g < s1; g += 8 * (int32_t)kWave) {
+                u32x4 jv = *(const lu128*)(jt + g);
+                uint64_t sp = *(const lu64*)(span + g);
+                uint32_t v[8], w[8], sb[8];
+                bool anyp = false;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int32_t i = g + q * (int32_t)kWave;
-                    v[q] = i < s1 ? jt[i] : kFinal;
+                for (int q = 0; q < 8; ++q) {
+                    v[q] = entry(jv, q, g);
+                    anyp |= v[q] < kCross;
+                }
+                if (!anyp) continue;  // (exec mask: only lanes with pointers read)
+                // unconditional reads (index 0 when unused): no branches
+                // between them, so all eight are in flight together
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const uint32_t x = jt[v[q] < kCross ? v[q] : 0u];
+                    w[q] = v[q] < kCross ? x : kFinal;
                 }
 #pragma unroll
-                for (int q = 0; q < 4; ++q) w[q] = v[q] < kCross ? jt[v[q]] : kFinal;
+                for (int q = 0; q < 8; ++q) sb[q] = span[v[q] < kCross ? v[q] : 0u];
+                bool any = false;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) sv[q] = (v[q] < kCross && w[q] == kFinal) ? span[v[q]] : 0u;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (v[q] < kCross) {
-                        const int32_t i = g + q * (int32_t)kWave;
-                        if (w[q] == kFinal) {
-                            span[i] = (uint8_t)sv[q];
-                            jt[i] = kFinal;
-                        } else {
-                            jt[i] = (uint16_t)w[q];
-                            more |= w[q] < kCross;
-                        }
-                    }
+                for (int q = 0; q < 8; ++q) {
+                    const bool ptr = v[q] < kCross, fin = w[q] == kFinal;
+                    any |= ptr;
+                    more |= ptr && w[q] < kCross;
+                    const uint32_t sh = 16 * (q & 1);
+                    const uint32_t cur = (jv[q >> 1] >> sh) & 0xFFFFu;
+                    const uint32_t ne = ptr ? w[q] : cur;
+                    jv[q >> 1] = (jv[q >> 1] & ~(0xFFFFu << sh)) | (ne << sh);
+                    const uint64_t bm = 0xFFull << (8 * q);
+                    sp = (ptr && fin) ? ((sp & ~bm) | ((uint64_t)(sb[q] & 0xFFu) << (8 * q))) : sp;
+                }
+                if (any) {
+                    *(lu64*)(span + g) = sp;
+                    *(lu128*)(jt + g) = jv;
                 }
             }
             wave_fence();
@@ -1119,21 +1147,33 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
         const int32_t lo1 = hdr[kHdrLo1], lo2 = hdr[kHdrLo2];
         const lu8* p1 = (const lu8*)S.span[(uint32_t)(j + kPipeSpans - 1) % kPipeSpans] - (lo1 & ~15);
         const lu8* p2 = (const lu8*)S.span[(uint32_t)(j + kPipeSpans - 2) % kPipeSpans] - (lo2 & ~15);
-        for (int32_t g = i0 + (int32_t)lane; g < s1; g += 4 * kWave) {
-            uint32_t v[4], x[4];
+        for (int32_t g = b0 + 8 * (int32_t)lane; g < s1; g += 8 * (int32_t)kWave) {
+            const u32x4 jv = *(const lu128*)(jt + g);
+            uint64_t sp = *(const lu64*)(span + g);
+            uint32_t x[8];
+            bool any = false;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int32_t i = g + q * (int32_t)kWave;
-                v[q] = i < s1 ? jt[i] : kFinal;
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t v = entry(jv, q, g);
+                any |= v != kFinal && v >= kCross;
+            }
+            if (!any) continue;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t v = entry(jv, q, g);
+                const bool cr = v != kFinal && v >= kCross;
+                const int32_t y = cr ? F + (int32_t)(v - kCross) : lo1;
+                x[q] = y >= lo1 ? p1[y] : p2[y];  // unconditional (p1[lo1] when unused)
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int32_t y = F + (int32_t)(v[q] - kCross);
-                x[q] = (v[q] != kFinal && v[q] >= kCross) ? (y >= lo1 ? p1[y] : p2[y]) : 0u;
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t v = entry(jv, q, g);
+                const bool cr = v != kFinal && v >= kCross;
+                any |= cr;
+                const uint64_t bm = 0xFFull << (8 * q);
+                sp = cr ? ((sp & ~bm) | ((uint64_t)(x[q] & 0xFFu) << (8 * q))) : sp;
             }
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (v[q] != kFinal && v[q] >= kCross) span[g + q * (int32_t)kWave] = (uint8_t)x[q];
+            if (any) *(lu64*)(span + g) = sp;
         }
         wave_fence();
     }
@@ -1162,15 +1202,19 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
 }
 
 // 6 workgroups (24 waves) per CU: 80 VGPRs and 19 KiB of LDS each.
+#ifndef LZ4E_PIPE_OCC
+#define LZ4E_PIPE_OCC 6
+#endif
 template <bool kStamps>
-__global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
+__global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_OCC) void decompress_pipe_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
     const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
-    uint64_t* __restrict__ dbg, const int32_t* __restrict__ dict_len) {
+    uint64_t* __restrict__ dbg, const int32_t* __restrict__ dict_len,
+    const uint32_t* __restrict__ order) {
     __shared__ __attribute__((aligned(16))) PipeLds S;
-    const uint32_t b = blockIdx.x;
-    if (b >= nblocks) return;
+    if (blockIdx.x >= nblocks) return;
+    const uint32_t b = order ? order[blockIdx.x] : blockIdx.x;
     const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
     const int32_t srcSize = src_len[b];
     const int32_t outSize = dst_cap[b];
@@ -1189,7 +1233,12 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
     }
     __syncthreads();
     PipeStamps st;
-    if (kStamps) st.t = clock64();
+    __shared__ uint64_t st_rows[kStamps ? kPipeWaves * kStSlots : 1];
+    if (kStamps) {
+        st.acc = st_rows + wave * kStSlots;
+        if (lane < kStSlots) st.acc[lane] = 0;
+        st.t = clock64();
+    }
 
     if (wave == 0) {
         // ---------------- parser ----------------
@@ -1270,7 +1319,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
             for (uint32_t q = 0; q < kHdrWords; ++q) hdr[q] = (int32_t)uni((uint32_t)S.hdr[slot][q]);
             bt.n = (uint32_t)hdr[kHdrN];
             lds_release(&S.con[slot], j);
-            if (kStamps) st.acc[kStBatches]++;
+            st.bump(kStamps, kStBatches);
             if (hdr[kHdrKind] == kKindHbm) {
                 // every earlier batch in HBM, then in place
                 if (!spin<kStamps>(S, [&] { return lds_acquire(&S.stored) >= hdr[kHdrLo]; }, st,
@@ -1302,6 +1351,43 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
 // blocks parse in a few batches; one wave each keeps more of them resident).
 constexpr uint32_t kPipeMinCap = 16384;
 
+// Launch order of the pipelined decoder when the batch takes more than one
+// round of workgroups: the kernel ends with its last block, so the heavy
+// blocks go first (longest-processing-time order).  A block's decode time
+// grows with its sequence count, estimated by its compressed size; frames
+// within 1/16 of their capacity (stored / incompressible data: a few long
+// literal runs) are the lightest.  64 buckets, one 1024-thread workgroup,
+// counting sort in LDS (order within a bucket is arbitrary: it only changes
+// which workgroup decodes which block).
+constexpr uint32_t kOrderBuckets = 64;
+constexpr uint32_t kOrderMin = 256 * 6;  // one round of pipelined workgroups
+constexpr uint32_t kOrderThreads = 1024;
+__global__ __launch_bounds__(kOrderThreads) void order_kernel(const int32_t* __restrict__ src_len,
+                                                     const int32_t* __restrict__ dst_cap,
+                                                     uint32_t nblocks, uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[kOrderBuckets], cur[kOrderBuckets];
+    const uint32_t t = threadIdx.x;
+    if (t < kOrderBuckets) hist[t] = 0;
+    __syncthreads();
+    auto bucket = [&](uint32_t b) -> uint32_t {
+        const int64_t c = src_len[b], cap = dst_cap[b];
+        if (cap <= 0 || c >= cap - cap / 16) return kOrderBuckets - 1;
+        const int64_t q = c <= 0 ? 0 : c * (kOrderBuckets - 1) / cap;  // < 63
+        return (uint32_t)(kOrderBuckets - 2 - (q < kOrderBuckets - 2 ? q : kOrderBuckets - 2));
+    };
+    for (uint32_t b = t; b < nblocks; b += kOrderThreads) atomicAdd(&hist[bucket(b)], 1u);
+    __syncthreads();
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (uint32_t k = 0; k < kOrderBuckets; ++k) {
+            cur[k] = acc;
+            acc += hist[k];
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = t; b < nblocks; b += kOrderThreads) order[atomicAdd(&cur[bucket(b)], 1u)] = b;
+}
+
 template <bool kStamps>
 hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* dbg) {
     if (a.nblocks == 0) return hipSuccess;
@@ -1311,10 +1397,23 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
     if (mode == kDecAuto && env) mode = env[0] == 'w' ? kDecWave : (env[0] == 'p' ? kDecPipe : kDecAuto);
     if (mode == kDecAuto) mode = (a.max_cap == 0 || a.max_cap >= kPipeMinCap) ? kDecPipe : kDecWave;
     if (mode == kDecPipe) {
+        // LZ4E_DECOMPRESS_ORDER=0 launches in block order (A/B experiments)
+        static const char* oenv = getenv("LZ4E_DECOMPRESS_ORDER");
+        uint32_t* order = nullptr;
+        if (a.nblocks > kOrderMin && !(oenv && oenv[0] == '0') &&
+            hipMallocAsync((void**)&order, sizeof(uint32_t) * a.nblocks, stream) == hipSuccess) {
+            hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kOrderThreads), 0, stream, a.src_len, a.dst_cap,
+                               a.nblocks, order);
+        } else {
+            (void)hipGetLastError();  // a failed pool allocation only costs the ordering
+            order = nullptr;
+        }
         hipLaunchKernelGGL((decompress_pipe_kernel<kStamps>), dim3(a.nblocks), dim3(kPipeWaves * kWave),
                            0, stream, a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.nblocks, dbg, a.dict_len);
-        return hipGetLastError();
+                           a.nblocks, dbg, a.dict_len, (const uint32_t*)order);
+        const hipError_t err = hipGetLastError();
+        if (order) (void)hipFreeAsync(order, stream);
+        return err;
     }
     hipLaunchKernelGGL((decompress_kernel<kStamps>), dim3(a.nblocks), dim3(kWave), 0, stream,
                        a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,

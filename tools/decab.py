@@ -22,7 +22,7 @@ P = ctypes.c_void_p
 L.lz4e_debug_decompress_stamped.argtypes = [P] * 7 + [ctypes.c_uint32, P, P, ctypes.c_uint32,
                                                        ctypes.c_uint32]
 PH = ["parse", "p_wait", "c_other", "c_rec", "c_far", "c_prev", "c_store", "batches", "c_loads",
-      "c_rounds", "c_gather", "c_spass", "c_vm", "n_rounds", "n_int", "unused"]
+      "c_rounds", "c_gather", "c_spass", "c_vm", "n_rounds", "n_int", "c_ptrs"]
 WAVE, PIPE = 1, 2
 
 
@@ -83,7 +83,7 @@ def run(kind, data, bs=65536, cls=1):
     print(f"== {kind:8s} {n} x {bs} ratio {ratio:.2f}: one-wave {ms[WAVE]:.3f} ms, pipelined "
           f"{ms[PIPE]:.3f} ms ({ms[WAVE] / ms[PIPE]:.2f}x)", flush=True)
     nb = max(1.0, d[:, 7].sum())
-    print("   per batch: " + "  ".join(f"{PH[i]} {d[:, i].sum() / nb:.0f}" for i in range(15) if i != 7)
+    print("   per batch: " + "  ".join(f"{PH[i]} {d[:, i].sum() / nb:.0f}" for i in range(16) if i != 7)
           + f"  (batches/block {d[:, 7].mean():.0f}, max {d[:, 7].max():.0f})", flush=True)
 
 
@@ -91,6 +91,14 @@ if __name__ == "__main__":
     nb = int(sys.argv[1]) if len(sys.argv) > 1 else 256
     for kind in ("text", "ints", "records", "runs", "random", "jpeg"):
         run(kind, blocks(kind, nb, 65536))
-    run("silesia", corpus.silesia_proxy(3234 * 65536, 0x5157))
+    sil = corpus.silesia_proxy(3234 * 65536, 0x5157)
+    run("silesia", sil)
+    if os.environ.get("DECAB_ORDER"):
+        # the same blocks, heaviest classes first (ints, records, text, runs, jpeg, random)
+        cls = np.random.default_rng(0x5157).choice(6, size=3234, p=[0.40, 0.15, 0.10, 0.10, 0.10, 0.15])
+        rank = np.array([2, 0, 3, 5, 4, 1])[cls]
+        order = np.argsort(rank, kind="stable")
+        run("sil-heavy1st", sil.reshape(3234, 65536)[order].reshape(-1))
+        run("sil-light1st", sil.reshape(3234, 65536)[order[::-1]].reshape(-1))
     run("text256k", corpus.text_proxy(953 * 262144, 7), 262144, 3)
     run("fio4k", corpus.fio_pattern(65536 * 4096), 4096)

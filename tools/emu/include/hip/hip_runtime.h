@@ -48,6 +48,10 @@ inline bool __syncthreads_or(int v) { return v != 0; }
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
     return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 }
+inline unsigned atomicAdd(unsigned* p, unsigned v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
+// (the decoder's launch order kernel is not emulated: no pool, block order)
+inline hipError_t hipMallocAsync(void**, size_t, hipStream_t) { return hipErrorOutOfMemory; }
+inline hipError_t hipFreeAsync(void*, hipStream_t) { return hipSuccess; }
 extern dim3 blockIdx;
 extern thread_local dim3 threadIdx;
 void emu_launch(uint32_t nblocks, std::function<void()> lane_body);
