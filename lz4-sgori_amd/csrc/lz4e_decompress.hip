@@ -42,6 +42,7 @@
 
 #include "lz4e_device.h"
 #include "lz4e_gpu.h"
+#include "lz4e_order.h"
 
 namespace lz4e {
 
@@ -1352,41 +1353,21 @@ __global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_OCC) void decompress_
 constexpr uint32_t kPipeMinCap = 16384;
 
 // Launch order of the pipelined decoder when the batch takes more than one
-// round of workgroups: the kernel ends with its last block, so the heavy
-// blocks go first (longest-processing-time order).  A block's decode time
-// grows with its sequence count, estimated by its compressed size; frames
-// within 1/16 of their capacity (stored / incompressible data: a few long
-// literal runs) are the lightest.  64 buckets, one 1024-thread workgroup,
-// counting sort in LDS (order within a bucket is arbitrary: it only changes
-// which workgroup decodes which block).
-constexpr uint32_t kOrderBuckets = 64;
+// round of workgroups (lz4e_order.h): a block's decode time grows with its
+// sequence count, estimated by its compressed size; frames within 1/16 of
+// their capacity (stored / incompressible data: a few long literal runs) are
+// the lightest.
 constexpr uint32_t kOrderMin = 256 * 6;  // one round of pipelined workgroups
-constexpr uint32_t kOrderThreads = 1024;
-__global__ __launch_bounds__(kOrderThreads) void order_kernel(const int32_t* __restrict__ src_len,
-                                                     const int32_t* __restrict__ dst_cap,
-                                                     uint32_t nblocks, uint32_t* __restrict__ order) {
-    __shared__ uint32_t hist[kOrderBuckets], cur[kOrderBuckets];
-    const uint32_t t = threadIdx.x;
-    if (t < kOrderBuckets) hist[t] = 0;
-    __syncthreads();
-    auto bucket = [&](uint32_t b) -> uint32_t {
+struct DecodeWeight {
+    const int32_t* src_len;
+    const int32_t* dst_cap;
+    LZ4E_DEV uint32_t operator()(uint32_t b) const {
         const int64_t c = src_len[b], cap = dst_cap[b];
         if (cap <= 0 || c >= cap - cap / 16) return kOrderBuckets - 1;
         const int64_t q = c <= 0 ? 0 : c * (kOrderBuckets - 1) / cap;  // < 63
         return (uint32_t)(kOrderBuckets - 2 - (q < kOrderBuckets - 2 ? q : kOrderBuckets - 2));
-    };
-    for (uint32_t b = t; b < nblocks; b += kOrderThreads) atomicAdd(&hist[bucket(b)], 1u);
-    __syncthreads();
-    if (t == 0) {
-        uint32_t acc = 0;
-        for (uint32_t k = 0; k < kOrderBuckets; ++k) {
-            cur[k] = acc;
-            acc += hist[k];
-        }
     }
-    __syncthreads();
-    for (uint32_t b = t; b < nblocks; b += kOrderThreads) order[atomicAdd(&cur[bucket(b)], 1u)] = b;
-}
+};
 
 template <bool kStamps>
 hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* dbg) {
@@ -1402,8 +1383,8 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
         uint32_t* order = nullptr;
         if (a.nblocks > kOrderMin && !(oenv && oenv[0] == '0') &&
             hipMallocAsync((void**)&order, sizeof(uint32_t) * a.nblocks, stream) == hipSuccess) {
-            hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kOrderThreads), 0, stream, a.src_len, a.dst_cap,
-                               a.nblocks, order);
+            hipLaunchKernelGGL((order_kernel<DecodeWeight>), dim3(1), dim3(kOrderThreads), 0, stream,
+                               DecodeWeight{a.src_len, a.dst_cap}, a.nblocks, order);
         } else {
             (void)hipGetLastError();  // a failed pool allocation only costs the ordering
             order = nullptr;

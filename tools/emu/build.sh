@@ -9,7 +9,7 @@ here=$(cd "$(dirname "$0")" && pwd)
 csrc="$here/../../lz4-sgori_amd/csrc"
 b="${EMU_BUILD:-$here/build}"
 mkdir -p "$b/src"
-cp "$csrc"/lz4e_compress.hip "$csrc"/lz4e_decompress.hip "$csrc"/lz4e_device.h "$csrc"/lz4e_gpu.h "$b/src/"
+cp "$csrc"/lz4e_compress.hip "$csrc"/lz4e_decompress.hip "$csrc"/lz4e_device.h "$csrc"/lz4e_gpu.h "$csrc"/lz4e_order.h "$b/src/"
 cp "$here/lz4e_wave.h" "$b/src/"
 cp "$here/emu.cpp" "$here/emu_dec.cpp" "$b/src/"
 CXX=${CXX:-/opt/rocm/llvm/bin/clang++}

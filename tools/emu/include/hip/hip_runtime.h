@@ -2,6 +2,7 @@
 // (tools/emu): just enough of the kernel language for lz4e_compress.hip to
 // compile as host C++, each lane a thread.  Never part of the product build.
 #pragma once
+#include <math.h>
 #include <stdint.h>
 #include <stddef.h>
 #include <stdlib.h>
@@ -49,6 +50,16 @@ inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v)
     return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 }
 inline unsigned atomicAdd(unsigned* p, unsigned v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
+inline float atomicAdd(float* p, float v) {
+    float o = *p, n = o + v;
+    while (!__atomic_compare_exchange(p, &o, &n, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) n = o + v;
+    return o;
+}
+inline unsigned atomicMin(unsigned* p, unsigned v) {
+    unsigned o = __atomic_load_n(p, __ATOMIC_RELAXED);
+    while (v < o && !__atomic_compare_exchange_n(p, &o, v, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
+    return o;
+}
 // (the decoder's launch order kernel is not emulated: no pool, block order)
 inline hipError_t hipMallocAsync(void**, size_t, hipStream_t) { return hipErrorOutOfMemory; }
 inline hipError_t hipFreeAsync(void*, hipStream_t) { return hipSuccess; }

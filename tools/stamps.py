@@ -67,6 +67,8 @@ def run(name, data, bs, cls, label):
         print(f"   {p:8s} {d[:, i].mean():12.0f}  ({100 * d[:, i].sum() / tot.sum():5.1f}%)")
     by_class(name, tot, n, lambda m: f"seq {seqs[m].mean():.0f} win {srch[m].mean():.0f} pass {rem[m].mean():.0f} att {fa[m].mean():.0f} fseq {fev[m].mean():.0f} " + " ".join(f"{ph[i]}={d[m, i].mean():.0f}" for i in range(6)))
     if name.startswith("silesia"):
+        os.makedirs("gpurun_out", exist_ok=True)
+        np.save(f"gpurun_out/stamps_{name}.npy", tot)  # per-block cycles (launch-order studies)
         cls = np.random.default_rng(0x5157).choice(6, size=n, p=[0.40, 0.15, 0.10, 0.10, 0.10, 0.15])
         top = np.argsort(-tot)[:12]
         print("   slowest blocks: " + ", ".join(f"{i}:{CLASS_NAMES[cls[i]]}:{tot[i] / 1e6:.2f}M" for i in top))
