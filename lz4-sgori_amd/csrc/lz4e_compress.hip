@@ -1148,7 +1148,6 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
 // silesia proxy its rank correlation with the measured parse cycles is
 // 0.85 (tools/comp_order.py measures the orders).
 constexpr uint32_t kWeightChunks = 16, kWeightChunk = 256, kWeightThreads = 256;
-constexpr uint32_t kWeightTable = 512;
 constexpr uint32_t kOrderMinBlocks = 1024;   // fewer: about one block per CU, nothing to spread
 constexpr uint32_t kOrderMinLen = 16384;     // small blocks finish in a few windows
 
@@ -1157,52 +1156,83 @@ __global__ __launch_bounds__(kWeightThreads) void weight_kernel(const uint8_t* _
                                                                 const uint32_t* __restrict__ src_len,
                                                                 uint32_t nblocks,
                                                                 uint32_t* __restrict__ weight) {
-    __shared__ uint32_t hist[256], tbl[kWeightTable], cnt[2];
-    __shared__ uint8_t chunk[kWeightChunk + 4];
+    // thread t: the 16 sample positions r0 .. r0 + 15 of chunk c; the
+    // chunks' first-occurrence tables (position per 8-bit hash) side by side
+    constexpr uint32_t kPer = kWeightChunks * kWeightChunk / kWeightThreads;  // 16
+    constexpr uint32_t kTab = 256;
+    __shared__ __attribute__((aligned(16))) uint8_t smp[kWeightChunks * kWeightChunk + 16];
+    __shared__ uint32_t hist[256], cnt[2], tbl[kWeightChunks * kTab];
     __shared__ float esum;
     const uint32_t b = blockIdx.x, t = threadIdx.x;
     if (b >= nblocks) return;
     const uint32_t n = src_len[b];
-    const uint8_t* in = src + src_off[b];
-    hist[t] = 0;
-    if (t < 2) cnt[t] = 0;
-    if (t == 0) esum = 0.f;
     if (n < kWeightChunk * 2) {
         if (t == 0) weight[b] = 0;
         return;
     }
-    for (uint32_t c = 0; c < kWeightChunks; ++c) {
-        const uint32_t base = (uint32_t)((uint64_t)(n - kWeightChunk) * c / (kWeightChunks - 1));
-        __syncthreads();
-        chunk[t] = in[base + t];
-        if (t < 4) chunk[kWeightChunk + t] = 0;
-        for (uint32_t i = t; i < kWeightTable; i += kWeightThreads) tbl[i] = ~0u;
-        __syncthreads();
-        atomicAdd(&hist[chunk[t]], 1u);
-        const bool has4 = t + 4 <= kWeightChunk;
-        const uint32_t w = chunk[t] | (chunk[t + 1] << 8) | (chunk[t + 2] << 16) | ((uint32_t)chunk[t + 3] << 24);
-        const uint32_t h = (w * 2654435761u) >> 23;  // 9 bits
-        if (has4) atomicMin(&tbl[h], t);
-        __syncthreads();
-        bool run = false, seen = false;
-        if (has4 && t >= 1) run = chunk[t - 1] == chunk[t] && w == (chunk[t] * 0x01010101u);
-        if (has4) {
-            const uint32_t f = tbl[h];
-            seen = f < t && (chunk[f] | (chunk[f + 1] << 8) | (chunk[f + 2] << 16) |
-                             ((uint32_t)chunk[f + 3] << 24)) == w;
-        }
-        const uint64_t rm = ballot(run), sm = ballot(seen);
-        if ((t & 63) == 0) {
-            atomicAdd(&cnt[0], popc64(rm));
-            atomicAdd(&cnt[1], popc64(sm));
+    const uint8_t* in = src + src_off[b];
+    const uint32_t c = t / (kWeightChunk / kPer), r0 = (t % (kWeightChunk / kPer)) * kPer;
+    const uint32_t base = (uint32_t)((uint64_t)(n - kWeightChunk) * c / (kWeightChunks - 1));
+    hist[t] = 0;
+    if (t < 2) cnt[t] = 0;
+    if (t == 0) esum = 0.f;
+    for (uint32_t i = t; i < kWeightChunks * kTab; i += kWeightThreads) tbl[i] = ~0u;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) smp[c * kWeightChunk + r0 + k] = in[base + r0 + k];
+    if (t < 16) smp[kWeightChunks * kWeightChunk + t] = 0;
+    __syncthreads();
+    const uint8_t* ch = smp + c * kWeightChunk;
+    const uint32_t* chw = (const uint32_t*)ch;  // 4-byte aligned (chunks of 256)
+    uint32_t* tb = tbl + c * kTab;
+    // my 16 positions' bytes (+ the 4 after) in registers: word k = bytes
+    // r0 + k .. r0 + k + 3
+    uint32_t d[kPer / 4 + 1];
+#pragma unroll
+    for (uint32_t i = 0; i <= kPer / 4; ++i) d[i] = chw[r0 / 4 + i];
+    const uint32_t prev = r0 ? ch[r0 - 1] : 0x100u;  // byte before my first position
+    auto word_at = [&](uint32_t r) -> uint32_t {  // any chunk offset (2 aligned reads)
+        return alignbyte(chw[r / 4 + 1], chw[r / 4], r & 3);
+    };
+    // No atomics on the sample's own values (runs and tables would put every
+    // lane of an instruction on one LDS address): every position writes its
+    // table slot and reads back the winner -- a word seen m times counts
+    // m - 1 positions, as "occurred earlier" would; the byte histogram takes
+    // every 4th byte.
+    uint32_t w[kPer];
+    uint32_t runs = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t r = r0 + k;
+        w[k] = alignbyte(d[k / 4 + 1], d[k / 4], k & 3);
+        if (k % 4 == 0) atomicAdd(&hist[w[k] & 0xFFu], 1u);
+        const uint32_t pb = k == 0 ? prev : (d[(k - 1) / 4] >> (8 * ((k - 1) & 3))) & 0xFFu;
+        if (r + 4 <= kWeightChunk) {
+            tb[(w[k] * 2654435761u) >> 24] = r;
+            runs += w[k] == pb * 0x01010101u;  // 5 equal bytes
         }
     }
     __syncthreads();
-    const float p = (float)hist[t] / (float)(kWeightChunks * kWeightChunk);
+    uint32_t seen = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kPer; ++k) {
+        const uint32_t r = r0 + k;
+        if (r + 4 <= kWeightChunk) {
+            const uint32_t f = tb[(w[k] * 2654435761u) >> 24];
+            seen += f != r && word_at(f) == w[k];
+        }
+    }
+    {
+        const uint32_t rs = wave_incl_add(runs), ss = wave_incl_add(seen);
+        if ((t & 63) == 63) {
+            atomicAdd(&cnt[0], rs);
+            atomicAdd(&cnt[1], ss);
+        }
+    }
+    const float p = (float)hist[t] / (float)(kWeightChunks * kWeightChunk / 4);
     if (p > 0.f) atomicAdd(&esum, -p * log2f(p));
     __syncthreads();
     if (t == 0) {
-        const float npos = (float)(kWeightChunks * (kWeightChunk - 4));
+        const float npos = (float)(kWeightChunks * (kWeightChunk - 3));
         const float R = (float)cnt[0] / npos, S = (float)cnt[1] / npos;
         weight[b] = esum > 7.5f ? 0u : (uint32_t)(1000.f * (1.f - R) * (0.2f + S));
     }
