@@ -1243,6 +1243,11 @@ __global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_OCC) void decompress_
 
     if (wave == 0) {
         // ---------------- parser ----------------
+        // (the critical path of the block: first in issue arbitration)
+#ifndef LZ4E_PARSER_PRIO
+#define LZ4E_PARSER_PRIO 3
+#endif
+        if (LZ4E_PARSER_PRIO) __builtin_amdgcn_s_setprio(LZ4E_PARSER_PRIO);
         Parse P;
         P.init(in, srcSize, outSize, (lu32*)S.ring, lane, dict_of(dict_len, b));
         int32_t j = 0, lo1 = 0, lo2 = 0, hi1 = 0, hi2 = 0;
