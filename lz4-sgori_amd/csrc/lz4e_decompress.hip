@@ -460,15 +460,20 @@ LZ4E_DEV void lane_copy64(lu8* dst, const uint8_t* src, int32_t len, const uint8
 
 // Byte x (< 256) of a 256-byte table held one dword per lane (ds_bpermute).
 LZ4E_DEV uint32_t table_at(uint32_t tab, uint32_t x) {
-    return (shfl(tab, x >> 2) >> ((x & 3) * 8)) & 0xFFu;
+    return (shfl_addr(tab, x & 0xFCu) >> ((x & 3) * 8)) & 0xFFu;
 }
 
-// The composed table B[A[p]] for this lane's 4 positions p.
+// The composed table B[A[p]] for this lane's 4 positions p: four gathers of
+// the source dwords (byte address = index & ~3), the wanted bytes picked and
+// packed by two v_perm_b32.
 LZ4E_DEV uint32_t table_compose(uint32_t A, uint32_t B) {
-    uint32_t r = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) r |= table_at(B, (A >> (8 * q)) & 0xFFu) << (8 * q);
-    return r;
+    const uint32_t a = A & 0xFCFCFCFCu;
+    const uint32_t g0 = shfl_addr(B, a & 0xFFu), g1 = shfl_addr(B, (a >> 8) & 0xFFu);
+    const uint32_t g2 = shfl_addr(B, (a >> 16) & 0xFFu), g3 = shfl_addr(B, a >> 24);
+    const uint32_t s = A & 0x03030303u;
+    const uint32_t r01 = perm_bytes(g1, g0, (s & 0xFFFFu) + 0x0C0C0400u);
+    const uint32_t r23 = perm_bytes(g3, g2, (s >> 16) + 0x0C0C0400u);
+    return r01 | (r23 << 16);
 }
 
 
@@ -519,7 +524,12 @@ enum ParseResult { kParsedFast, kParsedScalar, kParseFail };
 // kParsedScalar: one sequence of any length; kParseFail: malformed input or
 // too small a capacity, the return value is -(P.ip) - 1.  A fast batch's
 // output is at most cap_out (>= 32) bytes.
-LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_out = 64 * 32) {
+struct NoLap {
+    LZ4E_DEV void operator()(int) const {}
+};
+template <class Lap = NoLap>
+LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_out = 64 * 32,
+                                 Lap lap = Lap()) {
     const int32_t iend = P.iend, oend = P.oend;
     int32_t ip = P.ip, op = P.op;
     InWindow& win = P.win;
@@ -550,14 +560,17 @@ LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_
             }
             J[0] = j1;
         }
+        lap(0);
 #pragma unroll
         for (int i = 1; i < 6; ++i) J[i] = table_compose(J[i - 1], J[i - 1]);
+        lap(1);
         uint32_t x = 0;  // lane k: window offset of token k (255: past the chain)
 #pragma unroll
         for (int i = 0; i < 6; ++i) {
             const uint32_t y = table_at(J[i], x);
             x = (lane >> i) & 1 ? y : x;
         }
+        lap(2);
         const uint32_t t = table_at(wv, x);  // token byte
         const int32_t L = (int32_t)(t >> 4), Mt = (int32_t)(t & 15);
         const bool cand = x != 255 && L != 15 && Mt != 15 && (int32_t)x <= jlim;
@@ -586,6 +599,7 @@ LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_
             b.n = nf;
             P.op = op + lane_val((uint32_t)incl, nf - 1);
             P.ip = lane_val((uint32_t)(lp + L + 2), nf - 1);  // the token after the last one
+            lap(3);
             return kParsedFast;
         }
     }
@@ -979,7 +993,8 @@ LZ4E_DEV int32_t wave_min_i32(int32_t v) {
 // phases: loads + span setup, internal rounds, cross gather, store pass,
 // store completion; internal rounds, batches with internal pointers.
 enum { kStParse, kStPWait, kStWork, kStRec, kStFar, kStPrev, kStStore, kStBatches, kStLoads,
-       kStRounds, kStGather, kStSpass, kStVm, kStNRounds, kStNInt, kStUnused, kStSlots };
+       kStRounds, kStGather, kStSpass, kStVm, kStNRounds, kStNInt, kStUnused,
+       kStPWin, kStPComp, kStPFollow, kStPFields, kStSlots };
 // The accumulators live in LDS (a row per wave), so that the stamped build
 // has the register allocation of the real one.
 struct PipeStamps {
@@ -1067,7 +1082,7 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
     const bool has_int = ptrs && ss + b.M > lo;
     // rounds and gather start at the first pointer byte
     const int32_t i0 = (int32_t)uni((uint32_t)wave_min_i32(ptrs ? ms + nf - a0 : s1));
-    st.lap(kStamps, kStUnused);
+    st.lap(kStamps, kStUnused);  // (copier: pointer entries)
     // the loaded bytes into the span
     if (valid && b.L > 0) {
         if (lfast) put16(span + (b.op - a0), lv, (uint32_t)b.L, sink);
@@ -1255,7 +1270,9 @@ __global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_OCC) void decompress_
         for (;;) {
             Batch bt;
             const int32_t lo = P.op;
-            const ParseResult pr = parse_batch(P, bt, lane, kPipeOut);
+            const ParseResult pr = parse_batch(P, bt, lane, kPipeOut, [&](int k) {
+                if (kStamps) st.lap(true, kStPWin + k);
+            });
             st.lap(kStamps, kStParse);
             if (pr == kParseFail) {
                 if (lane == 0) ret[b] = -P.ip - 1;

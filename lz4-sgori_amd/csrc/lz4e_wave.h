@@ -70,6 +70,16 @@ LZ4E_DEV uint32_t push_lane(uint32_t v, uint32_t dst) {
 LZ4E_DEV void consume(uint32_t v) { asm volatile("" ::"v"(v)); }
 // ds_bpermute: lane src's value, per lane.
 LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return __shfl(v, (int)src); }
+// ds_bpermute with the byte address given (4 x source lane, mod 256): no
+// index arithmetic around it.
+LZ4E_DEV uint32_t shfl_addr(uint32_t v, uint32_t addr) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)addr, (int)v);
+}
+// v_perm_b32: byte i of the result is byte sel_i of {hi:lo} (0-3: lo, 4-7:
+// hi), 0 for a selector byte 0x0C.
+LZ4E_DEV uint32_t perm_bytes(uint32_t hi, uint32_t lo, uint32_t sel) {
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
 LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) { return __shfl_up(v, d); }
 // Inclusive prefix sum over the 64 lanes with DPP (row_shr 1/2/4/8 inside
 // each row of 16, then row_bcast:15 and row_bcast:31 across rows).

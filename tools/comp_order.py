@@ -22,6 +22,16 @@ inter = np.empty(N, dtype=np.int64)
 inter[0::2] = heavy[: (N + 1) // 2]
 inter[1::2] = heavy[::-1][: N // 2]
 orders = {"natural": np.arange(N), "heavy1st": heavy, "light1st": heavy[::-1], "interleaved": inter}
+if os.environ.get("COMP_ORDER_TIERS"):
+    # tiers of 1024 blocks (one per SIMD) by measured per-block cycles
+    # (tools/stamps.py output), alternately descending and ascending
+    cyc = np.load(os.path.join(REPO, "profiles", "r02", "stamps_silesia64k.npy"))
+    desc = np.argsort(-cyc, kind="stable")
+    T = 1024
+    snake = np.concatenate([desc[i:i + T] if (i // T) % 2 == 0 else desc[i:i + T][::-1]
+                            for i in range(0, N, T)])
+    pair = np.concatenate([desc[:T], desc[::-1][:T], desc[T:N - T]])
+    orders = {"measured-desc": desc, "snake": snake, "heavy+lightest": pair}
 cap = BS + BS // 255 + 16
 slot = (cap + 79) // 16 * 16
 offs = torch.arange(N, dtype=torch.int64, device=dev) * BS

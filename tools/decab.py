@@ -22,7 +22,9 @@ P = ctypes.c_void_p
 L.lz4e_debug_decompress_stamped.argtypes = [P] * 7 + [ctypes.c_uint32, P, P, ctypes.c_uint32,
                                                        ctypes.c_uint32]
 PH = ["parse", "p_wait", "c_other", "c_rec", "c_far", "c_prev", "c_store", "batches", "c_loads",
-      "c_rounds", "c_gather", "c_spass", "c_vm", "n_rounds", "n_int", "c_ptrs"]
+      "c_rounds", "c_gather", "c_spass", "c_vm", "n_rounds", "n_int", "c_ptrs",
+      "p_win", "p_comp", "p_follow", "p_fields"]
+NS = len(PH)
 WAVE, PIPE = 1, 2
 
 
@@ -53,7 +55,7 @@ def run(kind, data, bs=65536, cls=1):
     lz4e_amd.compress_batch_dev(src, offs, lens, tt, dst, doffs, caps, ret)
     out = torch.zeros(n * bs + 64, dtype=torch.uint8, device=dev)
     dret = torch.zeros(n, dtype=torch.int32, device=dev)
-    dbg = torch.zeros(n * 16, dtype=torch.int64, device=dev)
+    dbg = torch.zeros(n * NS, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream().cuda_stream
 
     def launch(mode, d=None):
@@ -78,12 +80,12 @@ def run(kind, data, bs=65536, cls=1):
     launch(PIPE, dbg.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(out[:n * bs], src)
-    d = dbg.cpu().numpy().reshape(n, 16).astype(np.float64)
+    d = dbg.cpu().numpy().reshape(n, NS).astype(np.float64)
     ratio = n * bs / ret.sum().item()
     print(f"== {kind:8s} {n} x {bs} ratio {ratio:.2f}: one-wave {ms[WAVE]:.3f} ms, pipelined "
           f"{ms[PIPE]:.3f} ms ({ms[WAVE] / ms[PIPE]:.2f}x)", flush=True)
     nb = max(1.0, d[:, 7].sum())
-    print("   per batch: " + "  ".join(f"{PH[i]} {d[:, i].sum() / nb:.0f}" for i in range(16) if i != 7)
+    print("   per batch: " + "  ".join(f"{PH[i]} {d[:, i].sum() / nb:.0f}" for i in range(NS) if i != 7)
           + f"  (batches/block {d[:, 7].mean():.0f}, max {d[:, 7].max():.0f})", flush=True)
 
 

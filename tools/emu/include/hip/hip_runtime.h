@@ -44,6 +44,7 @@ inline uint32_t atomicMax(uint32_t* p, uint32_t v) {
 #define __hip_atomic_load(p, order, scope) __atomic_load_n(p, order)
 #define __hip_atomic_store(p, v, order, scope) __atomic_store_n(p, v, order)
 #define __builtin_amdgcn_s_sleep(x) ((void)0)
+#define __builtin_amdgcn_s_setprio(x) ((void)0)
 inline void __syncthreads() {}
 inline bool __syncthreads_or(int v) { return v != 0; }
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {

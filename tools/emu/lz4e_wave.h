@@ -72,6 +72,19 @@ LZ4E_DEV uint32_t push_lane(uint32_t v, uint32_t dst) {
 }
 LZ4E_DEV void consume(uint32_t) {}
 LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return (uint32_t)emu_gather(v, src); }
+LZ4E_DEV uint32_t shfl_addr(uint32_t v, uint32_t addr) {
+    return (uint32_t)emu_gather(v, (addr >> 2) & 63);
+}
+LZ4E_DEV uint32_t perm_bytes(uint32_t hi, uint32_t lo, uint32_t sel) {
+    const uint64_t v = ((uint64_t)hi << 32) | lo;
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t s = (sel >> (8 * i)) & 0xFFu;
+        const uint32_t b = s < 8 ? (uint32_t)(v >> (8 * s)) & 0xFFu : 0u;  // (0x0C: 0)
+        r |= b << (8 * i);
+    }
+    return r;
+}
 LZ4E_DEV int32_t shfl_up(int32_t v, uint32_t d) {
     g_wave->slot[g_lane] = (uint32_t)v;
     g_wave->bar.arrive_and_wait();
