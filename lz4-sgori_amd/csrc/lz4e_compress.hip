@@ -349,7 +349,7 @@ LZ4E_DEV uint64_t lane_range(uint32_t a, uint32_t b) {
 template <int TT, bool kStamps, class IMG>
 LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* out, uint32_t cap,
                              int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg, uint32_t lane,
-                             uint32_t D = 0) {
+                             uint32_t D = 0, bool progress_prio = true) {
     // Dictionary mode (D > 0): the image is [D dictionary bytes | the n-byte
     // block], the parse starts at D and the table was preloaded from the
     // dictionary; positions are image positions throughout.
@@ -409,7 +409,7 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
         // Large blocks only: a batch's kernel time is its slowest block, and
         // raising the priority of the waves furthest behind shortens it
         // (silesia64k compress -9 %); 4 KiB blocks finish in a few windows.
-        uint32_t prio_q = n > 16384 ? 4 : 5;
+        uint32_t prio_q = (n > 16384 && progress_prio) ? 4 : 5;
         // Put pattern the clash fixpoint starts from for the lanes ahead of a
         // chain: every lane, or (periodic data: ints, records) the previous
         // window's final puts, whichever predicted the last window better.
@@ -1058,13 +1058,13 @@ LZ4E_DEV void stage_block(uint32_t* dstw, const uint8_t* src, uint32_t n, uint32
 template <bool kStamps, class IMG>
 LZ4E_DEV void dispatch_class(const IMG& img, uint32_t* smem, uint32_t n, int tt, gu8* out,
                              uint32_t cap, int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg,
-                             uint32_t lane, uint32_t D = 0) {
+                             uint32_t lane, uint32_t D = 0, bool pp = true) {
     if (tt == kByU32)
-        compress_block<kByU32, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, D);
+        compress_block<kByU32, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, D, pp);
     else if (tt == kByU16)
-        compress_block<kByU16, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane);
+        compress_block<kByU16, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, 0, pp);
     else
-        compress_block<kByU64, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane);
+        compress_block<kByU64, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, 0, pp);
 }
 
 template <bool kLdsInput, bool kStamps>
@@ -1132,7 +1132,12 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
                 atomicMax(&smem[hash_val<kByU32>(img.ld64(p))], p);
             block_sync();
         }
-        dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane, D);
+        // Issue priority: with a launch order the heavy blocks (its first two
+        // thirds) keep priority 3 for their whole parse and the light ones 0
+        // (silesia64k -4 %); without one, the waves furthest behind first.
+        const bool pp = order == nullptr;
+        if (order && blockIdx.x < (uint32_t)((uint64_t)nblocks * 2 / 3)) __builtin_amdgcn_s_setprio(3);
+        dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane, D, pp);
     }
 }
 
