@@ -1132,11 +1132,20 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
                 atomicMax(&smem[hash_val<kByU32>(img.ld64(p))], p);
             block_sync();
         }
-        // Issue priority: with a launch order the heavy blocks (its first two
-        // thirds) keep priority 3 for their whole parse and the light ones 0
-        // (silesia64k -4 %); without one, the waves furthest behind first.
-        const bool pp = order == nullptr;
-        if (order && blockIdx.x < (uint32_t)((uint64_t)nblocks * 2 / 3)) __builtin_amdgcn_s_setprio(3);
+        // Issue priority: the waves furthest behind first (progress
+        // priority, 3 -> 0 by quarter of the block), except in a batch that
+        // mixes heavy and light blocks (launch order with order[nblocks]
+        // heavy ones, kHeavyBucket, and at least 1/16 light): there the heavy
+        // blocks keep 3 for their whole parse and the light ones 0
+        // (silesia64k -4 %; text256k, all heavy, is 4 % faster with progress).
+        bool pp = true;
+        if (order) {
+            const uint32_t nh = order[nblocks];
+            if (nh < nblocks - nblocks / 16) {
+                pp = false;
+                if (blockIdx.x < nh) __builtin_amdgcn_s_setprio(3);
+            }
+        }
         dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane, D, pp);
     }
 }
@@ -1250,6 +1259,9 @@ struct CompressWeight {
         return (kOrderBuckets - 1) - (q < kOrderBuckets - 1 ? q : kOrderBuckets - 1);
     }
 };
+// Heavy blocks: weight >= 1200 * 7 / 63 ~ 133 (text ~290, tables and records
+// 400-470; long runs ~20, incompressible 0), i.e. bucket <= 56.
+constexpr uint32_t kHeavyBucket = kOrderBuckets - 1 - 7;
 
 uint32_t env_u32(const char* name, uint32_t dflt) {
     const char* e = getenv(name);
@@ -1275,11 +1287,12 @@ hipError_t launch_compress_impl(const CompressBatch& a, hipStream_t stream, uint
     static const uint32_t use_order = env_u32("LZ4E_COMPRESS_ORDER", 1);
     uint32_t* scratch = nullptr;
     if (use_order && a.nblocks >= kOrderMinBlocks && a.max_len >= kOrderMinLen &&
-        hipMallocAsync((void**)&scratch, sizeof(uint32_t) * 2 * (size_t)a.nblocks, stream) == hipSuccess) {
+        hipMallocAsync((void**)&scratch, sizeof(uint32_t) * (2 * (size_t)a.nblocks + 1), stream) == hipSuccess) {
         hipLaunchKernelGGL(weight_kernel, dim3(a.nblocks), dim3(kWeightThreads), 0, stream, a.src,
                            a.src_off, a.src_len, a.nblocks, scratch);
         hipLaunchKernelGGL((order_kernel<CompressWeight>), dim3(1), dim3(kOrderThreads), 0, stream,
-                           CompressWeight{scratch}, a.nblocks, scratch + a.nblocks);
+                           CompressWeight{scratch}, a.nblocks, scratch + a.nblocks, kHeavyBucket,
+                           scratch + 2 * (size_t)a.nblocks);
     } else {
         (void)hipGetLastError();  // a failed pool allocation only costs the ordering
         scratch = nullptr;

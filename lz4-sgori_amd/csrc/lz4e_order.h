@@ -21,9 +21,13 @@ namespace lz4e {
 constexpr uint32_t kOrderBuckets = 64;
 constexpr uint32_t kOrderThreads = 1024;
 
+// heavy (nullable): the number of blocks whose key is at most heavy_key (the
+// length of the launch order's heavy prefix).
 template <class Key>
 __global__ __launch_bounds__(kOrderThreads) void order_kernel(Key key, uint32_t nblocks,
-                                                              uint32_t* __restrict__ order) {
+                                                              uint32_t* __restrict__ order,
+                                                              uint32_t heavy_key = 0,
+                                                              uint32_t* __restrict__ heavy = nullptr) {
     __shared__ uint32_t hist[kOrderBuckets], cur[kOrderBuckets];
     const uint32_t t = threadIdx.x;
     if (t < kOrderBuckets) hist[t] = 0;
@@ -35,6 +39,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(Key key, uint32_t 
         for (uint32_t k = 0; k < kOrderBuckets; ++k) {
             cur[k] = acc;
             acc += hist[k];
+            if (heavy && k == heavy_key) *heavy = acc;
         }
     }
     __syncthreads();
