@@ -68,8 +68,11 @@ LZ4E_DEV uint32_t push_lane(uint32_t v, uint32_t dst) {
 // Keeps a value (e.g. a prefetch load's result) alive until here without
 // using it: the wait for it is placed here, not at the load.
 LZ4E_DEV void consume(uint32_t v) { asm volatile("" ::"v"(v)); }
-// ds_bpermute: lane src's value, per lane.
-LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) { return __shfl(v, (int)src); }
+// ds_bpermute: lane src's value (src mod 64), per lane.  (HIP's __shfl adds
+// the lane id and a width mask around it: two VALU more per shuffle.)
+LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((src & 63u) << 2), (int)v);
+}
 // ds_bpermute with the byte address given (4 x source lane, mod 256): no
 // index arithmetic around it.
 LZ4E_DEV uint32_t shfl_addr(uint32_t v, uint32_t addr) {
