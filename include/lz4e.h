@@ -184,7 +184,11 @@ int lz4e_decompress_batch(const char *const *src, const int *csize,
  * at most dst_cap[i] bytes at dst + dst_off[i]; ret[i] receives the block
  * size or 0.  `aux` (nullable, 2 words per block) receives
  * {final src position, last literal run} for iterator post-state.
- * `max_len` bounds src_len[] (it selects the LDS staging mode).
+ * `max_len` bounds src_len[] (it selects the LDS staging mode).  Batches
+ * of 1024+ blocks of 16 KiB+ are launched heaviest block first (a sampled
+ * weight per block and a counting sort on `stream`, scratch from the
+ * stream-ordered pool: hipMallocAsync / hipFreeAsync); the bytes written
+ * never depend on it.
  * Returns 0 on a successful launch, else a negative error.
  */
 int lz4e_compress_batch_dev(const uint8_t *src, const uint64_t *src_off,
@@ -200,7 +204,8 @@ int lz4e_compress_batch_dev(const uint8_t *src, const uint64_t *src_off,
  * dst_cap[] (0 = unknown): 16 KiB and more (or unknown) selects the
  * pipelined decoder (one parser wave and three copier waves per block),
  * smaller blocks decode on one wave each.  Both return identical values and
- * bytes.
+ * bytes.  Pipelined batches of more than 1536 blocks are launched in
+ * decreasing compressed-size order (as for compress, on `stream`).
  * Returns 0 on a successful launch, else a negative error.
  */
 int lz4e_decompress_batch_dev(const uint8_t *src, const uint64_t *src_off,
