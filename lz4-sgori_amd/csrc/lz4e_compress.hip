@@ -1282,11 +1282,12 @@ hipError_t launch_compress_impl(const CompressBatch& a, hipStream_t stream, uint
                            a.aux, a.nblocks, a.max_len, dbg, a.dict_len, nullptr);
         return hipGetLastError();
     }
-    // heavy blocks first (see weight_kernel); LZ4E_COMPRESS_ORDER=0 launches
-    // in block order (A/B experiments)
-    static const uint32_t use_order = env_u32("LZ4E_COMPRESS_ORDER", 1);
+    // heavy blocks first (see weight_kernel)
+    const int om = launch_order_mode(true);
+    const bool use_order = om == kOrderAlways ||
+                           (om == kOrderAuto && a.nblocks >= kOrderMinBlocks && a.max_len >= kOrderMinLen);
     uint32_t* scratch = nullptr;
-    if (use_order && a.nblocks >= kOrderMinBlocks && a.max_len >= kOrderMinLen &&
+    if (use_order &&
         hipMallocAsync((void**)&scratch, sizeof(uint32_t) * (2 * (size_t)a.nblocks + 1), stream) == hipSuccess) {
         hipLaunchKernelGGL(weight_kernel, dim3(a.nblocks), dim3(kWeightThreads), 0, stream, a.src,
                            a.src_off, a.src_len, a.nblocks, scratch);

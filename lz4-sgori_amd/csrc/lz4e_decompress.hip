@@ -1400,10 +1400,9 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
     if (mode == kDecAuto && env) mode = env[0] == 'w' ? kDecWave : (env[0] == 'p' ? kDecPipe : kDecAuto);
     if (mode == kDecAuto) mode = (a.max_cap == 0 || a.max_cap >= kPipeMinCap) ? kDecPipe : kDecWave;
     if (mode == kDecPipe) {
-        // LZ4E_DECOMPRESS_ORDER=0 launches in block order (A/B experiments)
-        static const char* oenv = getenv("LZ4E_DECOMPRESS_ORDER");
+        const int om = launch_order_mode(false);
         uint32_t* order = nullptr;
-        if (a.nblocks > kOrderMin && !(oenv && oenv[0] == '0') &&
+        if ((om == kOrderAlways || (om == kOrderAuto && a.nblocks > kOrderMin)) &&
             hipMallocAsync((void**)&order, sizeof(uint32_t) * a.nblocks, stream) == hipSuccess) {
             hipLaunchKernelGGL((order_kernel<DecodeWeight>), dim3(1), dim3(kOrderThreads), 0, stream,
                                DecodeWeight{a.src_len, a.dst_cap}, a.nblocks, order);

@@ -50,6 +50,13 @@ struct DecompressBatch {
 
 enum : uint32_t { kDecAuto = 0, kDecWave = 1, kDecPipe = 2 };
 
+// Launch order policy (lz4e_order.h): 0 block order, 1 heavy first when the
+// batch is large enough (default), 2 heavy first always.  From
+// lz4e_debug_set_launch_order, else LZ4E_COMPRESS_ORDER / LZ4E_DECOMPRESS_ORDER
+// (0 disables), else 1.
+enum : int { kOrderNever = 0, kOrderAuto = 1, kOrderAlways = 2 };
+int launch_order_mode(bool compress);
+
 uint32_t compress_lds_bytes(uint32_t max_len, bool lds_input);
 hipError_t launch_compress(const CompressBatch& a, hipStream_t stream);
 // Diagnostic build: per-block phase cycle counters (8 x u64 per block) into dbg.

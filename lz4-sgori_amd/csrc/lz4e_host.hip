@@ -815,6 +815,9 @@ uint64_t bio_vcnt_of_buffer(const char* data, uint32_t len) {
 // after this many sub-batches have been submitted (-1: never).
 std::atomic<int> g_chunk_fault_after{-1};
 
+// Launch order override per direction (compress, decompress): -1 default.
+std::atomic<int> g_order_override[2] = {{-1}, {-1}};
+
 // Waits for a slot's sub-batch and hands its results to the requests;
 // counts into `st` (this call's stats, added to the caller's on success).
 bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chunk_stats& st,
@@ -879,9 +882,26 @@ void chunk_drain(ChunkCtx& cc) {
 
 }  // namespace
 
+namespace lz4e {
+int launch_order_mode(bool compress) {
+    const int o = g_order_override[compress ? 0 : 1].load();
+    if (o >= kOrderNever && o <= kOrderAlways) return o;
+    const char* e = getenv(compress ? "LZ4E_COMPRESS_ORDER" : "LZ4E_DECOMPRESS_ORDER");
+    return (e && e[0] == '0') ? kOrderNever : kOrderAuto;
+}
+}  // namespace lz4e
+
 extern "C" {
 
 void lz4e_debug_chunk_fault_after(int subbatches) { g_chunk_fault_after.store(subbatches); }
+
+// Diagnostic: launch order policy of the device batches (lz4e_order.h) for
+// compress / decompress: -1 default (environment), 0 block order, 1 heavy
+// first for large batches, 2 heavy first always.  Results never depend on it.
+void lz4e_debug_set_launch_order(int compress_mode, int decompress_mode) {
+    g_order_override[0].store(compress_mode);
+    g_order_override[1].store(decompress_mode);
+}
 
 int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_chunk_stats* stats) {
     if (n <= 0) return 0;

@@ -823,3 +823,39 @@ def test_dict_streams_device_resident(gpu):
     torch.cuda.synchronize()
     assert (dret.cpu().numpy() == bs).all()
     assert np.array_equal(out[:n * bs].cpu().numpy(), host)
+
+
+# ---------------------------------------------------------------------------
+# launch order (lz4e_order.h): a schedule, never a result
+# ---------------------------------------------------------------------------
+
+@pytest.mark.parametrize("nblocks,bs", [(1100, 65536), (3, 65536), (1025, 16384)])
+def test_launch_order_does_not_change_results(gpu, nblocks, bs):
+    """Heavy-first launch order only decides which workgroup handles which
+    block: frames, iterator post-state, decoded bytes and return values are
+    identical in block order and in launch order (forced on for batches
+    below the size thresholds too), and equal the oracle's."""
+    L = gpu.lib()
+    L.lz4e_debug_set_launch_order.argtypes = [ctypes.c_int, ctypes.c_int]
+    data = _corpus("mixed", nblocks * bs, 23)
+    blocks = [data[i * bs:(i + 1) * bs].tobytes() for i in range(nblocks)]
+    # a few ragged blocks (the weight sample clamps, tiny blocks weigh 0)
+    blocks[1] = blocks[1][:700]
+    blocks[-1] = blocks[-1][:bs - 5]
+    ttypes = [BYU16] * nblocks
+    runs = {}
+    try:
+        for mode in (0, 2):
+            L.lz4e_debug_set_launch_order(mode, mode)
+            r, frames, aux = _gpu_compress(gpu, blocks, ttypes)
+            dr, dec = _gpu_decompress(gpu, frames, [bs] * nblocks, max_cap=bs)
+            runs[mode] = (r, frames, aux, dr, dec)
+    finally:
+        L.lz4e_debug_set_launch_order(-1, -1)
+    (r0, f0, a0, dr0, d0), (r2, f2, a2, dr2, d2) = runs[0], runs[2]
+    assert (r0 == r2).all() and f0 == f2 and (a0 == a2).all()
+    assert (dr0 == dr2).all() and d0 == d2
+    for i in range(0, nblocks, max(1, nblocks // 64)):
+        er, ef, efs, elr = oracle_ref.compress(blocks[i], BYU16)
+        assert (r2[i], f2[i], a2[i][0], a2[i][1]) == (er, ef, efs, elr), i
+        assert dr2[i] == len(blocks[i]) and d2[i] == blocks[i], i

@@ -16,6 +16,11 @@ alignas(16) uint32_t smem[(16384 + 65536 + 64) / 4];
 
 #include "lz4e_compress.hip"
 
+// The emulator launches in block order (no pool for the order's scratch).
+namespace lz4e {
+int launch_order_mode(bool) { return kOrderNever; }
+}  // namespace lz4e
+
 dim3 blockIdx;
 namespace lz4e {
 EmuWave* g_wave;
