@@ -80,6 +80,8 @@ def run(name, data, bs, cls, label):
 
 if __name__ == "__main__":
     mode = os.environ.get("LZ4E_COMPRESS_LDS_MAX", "default")
+    if os.environ.get("STAMPS_U32"):  # the sg512 workload's class (byU32)
+        run("silesia64k-u32", corpus.silesia_proxy(3234 * 65536, 0x5157), 65536, 3, f"lds_max={mode}")
     run("silesia64k", corpus.silesia_proxy(3234 * 65536, 0x5157), 65536, 1, f"lds_max={mode}")
     run("text64k", corpus.text_proxy(512 * 65536, 7), 65536, 1, f"lds_max={mode}")
     run("fio4k", corpus.fio_pattern(16384 * 4096), 4096, 1, f"lds_max={mode}")
