@@ -1217,7 +1217,7 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
     return true;
 }
 
-// 6 workgroups (24 waves) per CU: 80 VGPRs and 19 KiB of LDS each.
+// 6 workgroups (24 waves) per CU: 76 VGPRs and 19 KiB of LDS each.
 #ifndef LZ4E_PIPE_OCC
 #define LZ4E_PIPE_OCC 6
 #endif
