@@ -646,16 +646,6 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
                             const bool bad = ((U >> lane) & 1) && cg != cn &&
                                              (cg == 0 || cn == 0 ||
                                               __builtin_clzll(cg) != __builtin_clzll(cn));
-#ifdef LZ4E_EMU_TRACE
-                            {
-                                const uint64_t bm = ballot(bad);
-                                if (lane == 0)
-                                    printf("W B=%u ks=%u pass=%u k=%u Pg=%016llx Pn=%016llx U=%016llx bad=%016llx g=%016llx clash=%016llx\n",
-                                           B, ks, pass, k, (unsigned long long)Pg, (unsigned long long)Pn,
-                                           (unsigned long long)U, (unsigned long long)bm,
-                                           (unsigned long long)guess, (unsigned long long)clash);
-                            }
-#endif
                             if (!ballot(bad)) break;  // fixpoint
                             if (pass + 1 == kMaxPass) {          // give up: exact walk
                                 nev = 0;

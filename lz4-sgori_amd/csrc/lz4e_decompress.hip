@@ -987,13 +987,14 @@ LZ4E_DEV int32_t wave_min_i32(int32_t v) {
 }
 
 
-// Cycle counters of the stamped build, per block (u64 x 16): parser parse,
+// Cycle counters of the stamped build, per block (u64 x 20): parser parse,
 // parser waits, copier other work, copier waits for records, for far loads,
 // for batch j-1 (resolved), for the in-order store flag, batches; copier
 // phases: loads + span setup, internal rounds, cross gather, store pass,
-// store completion; internal rounds, batches with internal pointers.
+// store completion; internal rounds, batches with internal pointers; copier
+// pointer entries; parser phases: window, table composition, follow, fields.
 enum { kStParse, kStPWait, kStWork, kStRec, kStFar, kStPrev, kStStore, kStBatches, kStLoads,
-       kStRounds, kStGather, kStSpass, kStVm, kStNRounds, kStNInt, kStUnused,
+       kStRounds, kStGather, kStSpass, kStVm, kStNRounds, kStNInt, kStPtrs,
        kStPWin, kStPComp, kStPFollow, kStPFields, kStSlots };
 // The accumulators live in LDS (a row per wave), so that the stamped build
 // has the register allocation of the real one.
@@ -1082,7 +1083,7 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
     const bool has_int = ptrs && ss + b.M > lo;
     // rounds and gather start at the first pointer byte
     const int32_t i0 = (int32_t)uni((uint32_t)wave_min_i32(ptrs ? ms + nf - a0 : s1));
-    st.lap(kStamps, kStUnused);  // (copier: pointer entries)
+    st.lap(kStamps, kStPtrs);
     // the loaded bytes into the span
     if (valid && b.L > 0) {
         if (lfast) put16(span + (b.op - a0), lv, (uint32_t)b.L, sink);
@@ -1218,11 +1219,8 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
 }
 
 // 6 workgroups (24 waves) per CU: 76 VGPRs and 19 KiB of LDS each.
-#ifndef LZ4E_PIPE_OCC
-#define LZ4E_PIPE_OCC 6
-#endif
 template <bool kStamps>
-__global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_OCC) void decompress_pipe_kernel(
+__global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
     const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
@@ -1259,10 +1257,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_OCC) void decompress_
     if (wave == 0) {
         // ---------------- parser ----------------
         // (the critical path of the block: first in issue arbitration)
-#ifndef LZ4E_PARSER_PRIO
-#define LZ4E_PARSER_PRIO 3
-#endif
-        if (LZ4E_PARSER_PRIO) __builtin_amdgcn_s_setprio(LZ4E_PARSER_PRIO);
+        __builtin_amdgcn_s_setprio(3);
         Parse P;
         P.init(in, srcSize, outSize, (lu32*)S.ring, lane, dict_of(dict_len, b));
         int32_t j = 0, lo1 = 0, lo2 = 0, hi1 = 0, hi2 = 0;
