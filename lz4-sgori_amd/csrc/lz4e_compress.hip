@@ -409,7 +409,11 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
         // Large blocks only: a batch's kernel time is its slowest block, and
         // raising the priority of the waves furthest behind shortens it
         // (silesia64k compress -9 %); 4 KiB blocks finish in a few windows.
+        // q = floor(4 (e - D) / n) moves only at the quarter marks, so the
+        // window loop compares e against the next mark (a division per
+        // window costs ~25 instructions and two VALU -> SALU hops).
         uint32_t prio_q = (n > 16384 && progress_prio) ? 4 : 5;
+        uint32_t prio_next = prio_q == 5 ? ~0u : D;  // e - D at which q changes next
         // Put pattern the clash fixpoint starts from for the lanes ahead of a
         // chain: every lane, or (periodic data: ints, records) the previous
         // window's final puts, whichever predicted the last window better.
@@ -426,8 +430,9 @@ LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* ou
         };
         for (;;) {
             // ================= window setup =================================
-            if (prio_q != 5) {
+            if (e >= prio_next) {
                 const uint32_t q = (uint32_t)(((uint64_t)(e - D) * 4) / n);
+                prio_next = q >= 4 ? ~0u : D + (uint32_t)(((uint64_t)(q + 1) * n + 3) / 4);
                 if (q != prio_q) {
                     prio_q = q;
                     wave_prio_for(q);
