@@ -193,7 +193,20 @@ template <class IMG>
 LZ4E_DEV void out_copy(gu8* out, uint32_t at, const IMG& img, uint32_t from, uint32_t len,
                        uint32_t lane) {
     constexpr uint32_t kChunk = 4 * 4 * kWave;
-    for (uint32_t base = 0; base < len; base += kChunk) {
+    // Long runs (incompressible data, last literals): 2 KiB per round trip.
+    // A wave's loads wait behind its earlier stores (one in-order vmcnt), so
+    // the copy costs one HBM round trip per chunk; 1 KiB chunks held
+    // incompressible 64 KiB blocks at ~0.5 byte per cycle.
+    constexpr uint32_t kBig = 2 * kChunk;
+    uint32_t base = 0;
+    for (; base + kBig <= len; base += kBig) {
+        uint32_t w[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) w[j] = img.ld32(from + base + 4 * (j * kWave + lane));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) st32(out, at + base + 4 * (j * kWave + lane), w[j]);
+    }
+    for (; base < len; base += kChunk) {
         uint32_t w[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
