@@ -125,6 +125,31 @@ struct InWindow {
         const uint32_t w = r < 256 ? lane_val(a, r >> 2) : lane_val(b, (r - 256) >> 2);
         return (w >> ((r & 3) * 8)) & 0xFFu;
     }
+    // Length-extension scan, 256 bytes per step: the first block position
+    // q >= p0 whose byte is not 255 or that is >= plim (the reference reads
+    // such runs one byte at a time, lz4e_decompress.c:201-206, 319-326; a
+    // byte at a time cost one v_readlane round trip each).  Bytes past the
+    // block read as the clamped last word, never past q's decision: q <= plim
+    // and plim lies inside the block.
+    LZ4E_DEV int32_t ext_stop(int32_t p0, int32_t plim) {
+        for (int32_t p = p0;;) {
+            follow(p);  // p in window A = [base, base + 256)
+            const int32_t pa = base + 4 * (int32_t)lane;
+            uint32_t m = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t) {
+                const int32_t q = pa + (int32_t)t;
+                const bool stop = q >= p && (((a >> (8 * t)) & 0xFFu) != 0xFFu || q >= plim);
+                m |= (stop ? 1u : 0u) << t;
+            }
+            const uint64_t bm = ballot(m != 0);
+            if (bm) {
+                const uint32_t l = ctz64(bm);
+                return base + 4 * (int32_t)l + (int32_t)__builtin_ctz(lane_val(m, l));
+            }
+            p = base + 256;
+        }
+    }
     // Byte at window offset r (< 512), no range check.
     LZ4E_DEV uint32_t ubyte(uint32_t r) const {
         const uint32_t w = r < 256 ? lane_val(a, r >> 2) : lane_val(b, (r - 256) >> 2);
@@ -280,8 +305,24 @@ LZ4E_DEV void lane_match(uint8_t* dst, uint32_t off, int32_t len, const uint8_t*
 }
 
 // Whole-wave copy of len literal bytes (non-overlapping), 16 B per lane.
+// With kU > 1 long runs move kU KiB per HBM round trip: a wave's loads wait
+// behind its earlier stores (one in-order vmcnt), so 1 KiB steps hold an
+// incompressible block's copy at one round trip per KiB.  (The pipelined
+// decoder uses 4; the one-wave decoder keeps 1: 16 more VGPRs would cost it
+// a wave per SIMD.)
+template <int kU = 1>
 LZ4E_DEV void wave_copy(uint8_t* dst, const uint8_t* src, int32_t len, uint32_t lane) {
+    constexpr int32_t kStep = 16 * kWave;
     int32_t k = 16 * (int32_t)lane;
+    if constexpr (kU > 1) {
+        for (; k + (kU - 1) * kStep + 16 <= len; k += kU * kStep) {
+            uint4 v[kU];
+#pragma unroll
+            for (int j = 0; j < kU; ++j) v[j] = *reinterpret_cast<const uint4*>(src + k + j * kStep);
+#pragma unroll
+            for (int j = 0; j < kU; ++j) *reinterpret_cast<uint4*>(dst + k + j * kStep) = v[j];
+        }
+    }
     for (; k + 16 <= len; k += 16 * kWave)
         *reinterpret_cast<uint4*>(dst + k) = *reinterpret_cast<const uint4*>(src + k);
     for (int32_t t = (len & ~15) + lane; t < len; t += kWave) dst[t] = src[t];
@@ -527,7 +568,10 @@ enum ParseResult { kParsedFast, kParsedScalar, kParseFail };
 struct NoLap {
     LZ4E_DEV void operator()(int) const {}
 };
-template <class Lap = NoLap>
+// kVecExt: length-extension runs by 256-byte vector scans (the pipelined
+// decoder; the one-wave decoder keeps the byte loop: 2 more VGPRs would cost
+// it a wave per SIMD, and its <= 16 KiB blocks hold short runs).
+template <bool kVecExt = false, class Lap = NoLap>
 LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_out = 64 * 32,
                                  Lap lap = Lap()) {
     const int32_t iend = P.iend, oend = P.oend;
@@ -632,12 +676,21 @@ LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_
     }
     if (length == 15) {  // :194-220
         if (ip >= iend - 15) goto fail;
-        uint32_t s;
-        do {
-            s = win.byte(ip);
-            ip++;
-            length = length + s > kSat ? kSat : length + s;
-        } while (ip < iend - 15 && s == 255);
+        if constexpr (kVecExt) {
+            // bytes ip .. q: 255 each, then s; the loop goes on while the
+            // next position is below iend - 15
+            const int32_t q = win.ext_stop(ip, iend - 16);
+            const uint64_t sum = (uint64_t)length + 255ull * (uint64_t)(q - ip) + win.byte(q);
+            length = sum > kSat ? kSat : (uint32_t)sum;
+            ip = q + 1;
+        } else {
+            uint32_t s;
+            do {
+                s = win.byte(ip);
+                ip++;
+                length = length + s > kSat ? kSat : length + s;
+            } while (ip < iend - 15 && s == 255);
+        }
     }
     {
         const uint32_t cpy = (uint32_t)op + length;  // :223-288
@@ -665,13 +718,26 @@ copy_match_checks:
     // up to D bytes before the output (:299-302, checkOffset)
     if (op - offset + P.D < 0) goto fail;
     if (length == 15) {
-        uint32_t s;
-        do {
-            s = win.byte(ip);
-            ip++;
-            if (ip > iend - 5) goto fail;
-            length = length + s > kSat ? kSat : length + s;
-        } while (s == 255);
+        // bytes ip .. q: 255 each, then s; reading a byte at or past
+        // iend - 5 fails (ip > iend - 5 after the read)
+        if constexpr (kVecExt) {
+            const int32_t q = win.ext_stop(ip, iend - 5);
+            if (q + 1 > iend - 5) {
+                ip = q + 1;
+                goto fail;
+            }
+            const uint64_t sum = (uint64_t)length + 255ull * (uint64_t)(q - ip) + win.byte(q);
+            length = sum > kSat ? kSat : (uint32_t)sum;
+            ip = q + 1;
+        } else {
+            uint32_t s;
+            do {
+                s = win.byte(ip);
+                ip++;
+                if (ip > iend - 5) goto fail;
+                length = length + s > kSat ? kSat : length + s;
+            } while (s == 255);
+        }
     }
     if (ugt((uint32_t)op + length + 4, oend - 5)) goto fail;
     length += 4;
@@ -700,6 +766,7 @@ fail:
 // literal run, then the match; same-wave stores and loads to one global
 // address are ordered by the hardware (one vector L1 per CU) and the
 // wavefront fences keep the compiler from moving loads above the stores.
+template <int kU = 1>
 LZ4E_DEV void copy_scalar_hbm(const Batch& b, const uint8_t* in, int32_t srcSize, uint8_t* gout,
                               int32_t outSize, uint32_t lane) {
     const int32_t L = lane_val((uint32_t)b.L, 0), op = lane_val((uint32_t)b.op, 0);
@@ -709,7 +776,7 @@ LZ4E_DEV void copy_scalar_hbm(const Batch& b, const uint8_t* in, int32_t srcSize
     if (L > 0 && L <= kLong) {
         if (lane == 0) lane_copy64(gout + op, in + ls, L, in + srcSize);
     } else if (L > kLong) {
-        wave_copy(gout + op, in + ls, L, lane);
+        wave_copy<kU>(gout + op, in + ls, L, lane);
     }
     wave_fence();
     const int32_t ms = op + L;
@@ -1265,7 +1332,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
         for (;;) {
             Batch bt;
             const int32_t lo = P.op;
-            const ParseResult pr = parse_batch(P, bt, lane, kPipeOut, [&](int k) {
+            const ParseResult pr = parse_batch<true>(P, bt, lane, kPipeOut, [&](int k) {
                 if (kStamps) st.lap(true, kStPWin + k);
             });
             st.lap(kStamps, kStParse);
@@ -1345,7 +1412,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
                     if (lane == 0) ret[b] = kPipeAbort;
                     break;
                 }
-                copy_scalar_hbm(bt, in, srcSize, gout, outSize, lane);
+                copy_scalar_hbm<4>(bt, in, srcSize, gout, outSize, lane);
                 stores_done();
                 lds_release(&S.resolved, j + 1);
                 lds_release(&S.stored, hdr[kHdrHi]);
