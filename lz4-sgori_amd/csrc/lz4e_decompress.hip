@@ -571,6 +571,13 @@ struct NoLap {
 // kVecExt: length-extension runs by 256-byte vector scans (the pipelined
 // decoder; the one-wave decoder keeps the byte loop: 2 more VGPRs would cost
 // it a wave per SIMD, and its <= 16 KiB blocks hold short runs).
+// The one-wave decoder's choice; the CPU lane emulator's test build turns it
+// on (-DLZ4E_ONEWAVE_VEC_EXT=true) so that the vector scan runs under ASan
+// against the oracle (tests/test_emulator.py).
+#ifndef LZ4E_ONEWAVE_VEC_EXT
+#define LZ4E_ONEWAVE_VEC_EXT false
+#endif
+constexpr bool kOneWaveVecExt = LZ4E_ONEWAVE_VEC_EXT;
 template <bool kVecExt = false, class Lap = NoLap>
 LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_out = 64 * 32,
                                  Lap lap = Lap()) {
@@ -813,7 +820,7 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
 
     for (;;) {
         Batch b;
-        const ParseResult pr = parse_batch(P, b, lane);
+        const ParseResult pr = parse_batch<kOneWaveVecExt>(P, b, lane);
         if (pr == kParseFail) {
             if (lane == 0) *ret_slot = -P.ip - 1;
             break;

@@ -23,18 +23,32 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CXX = "/opt/rocm/llvm/bin/clang++"
 
 
-@pytest.fixture(scope="session")
-def emu_exe(tmp_path_factory):
+def _build_emu(tmp_path_factory, *extra):
     if not os.path.exists(CXX):
         pytest.skip("no clang++ for the emulator")
     b = tmp_path_factory.mktemp("emu")
     env = dict(os.environ, EMU_EXE="1", EMU_BUILD=str(b), CXX=CXX)
     subprocess.run(["bash", os.path.join(REPO, "tools", "emu", "build.sh"),
                     "-fsanitize=address,undefined", "-fno-sanitize=alignment",
-                    "-fno-sanitize-recover=all"], check=True, env=env, capture_output=True)
+                    "-fno-sanitize-recover=all", *extra], check=True, env=env, capture_output=True)
     exe = b / "emu_main"
     assert exe.exists()
-    yield str(exe)
+    return b, str(exe)
+
+
+@pytest.fixture(scope="session")
+def emu_exe(tmp_path_factory):
+    b, exe = _build_emu(tmp_path_factory)
+    yield exe
+    shutil.rmtree(b, ignore_errors=True)
+
+
+@pytest.fixture(scope="session")
+def emu_exe_vecext(tmp_path_factory):
+    """The decoder built with the pipelined decoder's vector length-extension
+    scan (InWindow::ext_stop) in the one-wave parse."""
+    b, exe = _build_emu(tmp_path_factory, "-DLZ4E_ONEWAVE_VEC_EXT=true")
+    yield exe
     shutil.rmtree(b, ignore_errors=True)
 
 
@@ -152,3 +166,57 @@ def test_emulated_decoder_sanitized(emu_exe, tmp_path, kind, mode):
         assert got[0] == want[0], (rep, got[0], want[0])
         if want[0] >= 0:
             assert got[1] == want[1], rep
+
+
+VEC_CASES = [(k, m) for k in ("random", "runs", "text") for m in range(4)]
+
+
+@pytest.mark.parametrize("kind,mode", VEC_CASES, ids=[f"{k}-{m}" for k, m in VEC_CASES])
+def test_emulated_decoder_vector_extension_scan(emu_exe_vecext, tmp_path, kind, mode):
+    """The length-extension scan (one ballot per 256 window bytes instead of
+    the reference's byte loop, lz4e_decompress.c:201-206, 319-326): values,
+    error codes and bytes equal the oracle's on valid frames (mode 0),
+    truncations (1), bit flips (2) and short capacity (3); random data gives
+    literal runs with extensions of up to ~100 bytes, runs long match
+    extensions."""
+    rng = np.random.default_rng(300 + mode)
+    for rep in range(3):
+        n = int(rng.integers(5000, 26000))
+        blk = _block(kind, n, 5 + rep + n).tobytes()
+        f = oracle_ref.compress(blk, BYU16)[1]
+        cap = len(blk)
+        if mode == 1:
+            f = f[:int(rng.integers(1, len(f)))]
+        elif mode == 2:
+            fb = bytearray(f)
+            for _ in range(3):
+                fb[int(rng.integers(0, len(fb)))] ^= 1 << int(rng.integers(0, 8))
+            f = bytes(fb)
+        elif mode == 3:
+            cap = max(0, cap - int(rng.integers(1, 40)))
+        want = oracle_ref.decompress_dict(f, cap, b"")
+        got = _emu_decode(emu_exe_vecext, tmp_path, f, cap)
+        assert got[0] == want[0], (rep, got[0], want[0])
+        if want[0] >= 0:
+            assert got[1] == want[1], rep
+
+
+def test_emulated_decoder_vector_extension_truncated_in_run(emu_exe_vecext, tmp_path):
+    """Frames cut inside and just after a literal-length extension run (the
+    reference's end checks on the run, lz4e_decompress.c:197-206), and an
+    extension run whose 255 bytes reach the frame end."""
+    blk = _block("random", 20000, 77).tobytes()
+    f = oracle_ref.compress(blk, BYU16)[1]
+    ext = 1
+    while f[ext] == 255:
+        ext += 1
+    cuts = sorted({1, 2, 3, ext - 1, ext, ext + 1, ext + 2, ext + 15, ext + 16, ext + 17, ext + 40})
+    for k in cuts:
+        ff = f[:k]
+        want = oracle_ref.decompress_dict(ff, len(blk), b"")
+        got = _emu_decode(emu_exe_vecext, tmp_path, ff, len(blk))
+        assert got[0] == want[0], (k, got[0], want[0])
+    ff = bytes([0xF0]) + b"\xff" * 300
+    want = oracle_ref.decompress_dict(ff, 100000, b"")
+    got = _emu_decode(emu_exe_vecext, tmp_path, ff, 100000)
+    assert got[0] == want[0], (got[0], want[0])

@@ -50,6 +50,9 @@ static int decode_main(int argc, char** argv) {
     const uint64_t so = 0, doff = (uint64_t)D;
     int32_t ret = -7777;
     if (frame.empty()) frame.push_back(0);  // a valid pointer for csize 0
+    // the decoder reads the input window by aligned dwords (the GPU's word
+    // granularity: the dword holding the last byte); the heap block covers it
+    frame.reserve((frame.size() + 3) & ~(size_t)3);
     emu_decompress_batch(frame.data(), &so, &csize, out.data(), &doff, &cap, &ret, 1, &D);
     printf("ret %d\n", ret);
     if (argc > 4 && ret > 0) {
