@@ -207,12 +207,31 @@ int lz4e_compress_batch_dev(const uint8_t *src, const uint64_t *src_off,
  * bytes.  Pipelined batches of more than 1536 blocks are launched in
  * decreasing compressed-size order (as for compress, on `stream`).
  * Returns 0 on a successful launch, else a negative error.
+ *
+ * ret[i] == LZ4E_DECODE_ABORTED: the pipelined decoder's watchdog fired
+ * (one of its waves waited ~1 s while nothing it depends on moved: a broken
+ * invariant of the decoder, never a property of the input).  The reference
+ * has no such outcome (lz4e_decompress.c:449-459 returns bytes written or
+ * -(ip - src) - 1); the host entry points turn it into a failed call:
+ * lz4e_decompress_batch / _dict / _sg_batch return -1, LZ4E_decompress_safe
+ * (and _usingDict / lz4e_decompress_safe_sg) return LZ4E_DECODE_ABORTED,
+ * lz4e_chunk_write_batch returns -1, each with lz4e_last_error() saying so.
+ * (A genuine -(ip - src) - 1 equals it only for ip = 2^31 - 1, an input the
+ * 0x7E000000-byte block limit cannot produce.)
+ *
+ * lz4e_decompress_batch_dev2 is the current form; lz4e_decompress_batch_dev
+ * keeps the round-1 signature (no max_cap: pipelined decoder throughout).
  */
+#define LZ4E_DECODE_ABORTED (-2147483647 - 1)
+int lz4e_decompress_batch_dev2(const uint8_t *src, const uint64_t *src_off,
+			       const int32_t *src_len, uint8_t *dst,
+			       const uint64_t *dst_off, const int32_t *dst_cap,
+			       int32_t *ret, uint32_t nblocks, uint32_t max_cap,
+			       void *stream);
 int lz4e_decompress_batch_dev(const uint8_t *src, const uint64_t *src_off,
 			      const int32_t *src_len, uint8_t *dst,
 			      const uint64_t *dst_off, const int32_t *dst_cap,
-			      int32_t *ret, uint32_t nblocks, uint32_t max_cap,
-			      void *stream);
+			      int32_t *ret, uint32_t nblocks, void *stream);
 
 /*
  * Dictionary mode.  The reference stubs its dictionary
@@ -319,12 +338,19 @@ struct lz4e_chunk_request {
 
 /* Write-side counters, the reference's struct lz4e_stats
  * (lz4e_bdev/include/lz4e_stats.h:17-22) updated as lz4e_stats_update does
- * at bio completion (lz4e_bdev/lz4e_stats.c:39-52): every request counts in
- * reqs_total, a failed one in reqs_failed only; a successful one adds the
- * bi_vcnt of the bio the reference completes (its src buffer re-added by
+ * at bio completion (lz4e_bdev/lz4e_stats.c:39-52), which only runs from
+ * lz4e_end_io (lz4e_req.c:231-246): only a request whose round trip
+ * completed (status 0) counts.  It adds 1 to reqs_total, the bi_vcnt of the
+ * bio the reference completes (its src buffer re-added by
  * lz4e_add_buf_to_bio, lz4e_req.c:191-197: one merged bio_vec per
  * contiguous non-empty buffer) to vec_count and its size to data_in_bytes.
- * frame_bytes (not in the reference) = sum of comp_size. */
+ * A request that fails in the write path (-EIO: compress or decompress
+ * failure, more than 256 segments, oversize; -ENOSPC) returns through
+ * lz4e_dev.c:187-202 in the reference and touches no counter.
+ * reqs_failed counts completed bios the underlying device failed
+ * (lz4e_stats.c:43-45); this library has no underlying device, so it is
+ * always 0.  frame_bytes (not in the reference) = sum of comp_size of the
+ * counted requests. */
 struct lz4e_chunk_stats {
 	uint64_t reqs_total;
 	uint64_t reqs_failed;

@@ -310,8 +310,15 @@ LZ4E_DEV void lane_match(uint8_t* dst, uint32_t off, int32_t len, const uint8_t*
 // incompressible block's copy at one round trip per KiB.  (The pipelined
 // decoder uses 4; the one-wave decoder keeps 1: 16 more VGPRs would cost it
 // a wave per SIMD.)
-template <int kU = 1>
-LZ4E_DEV void wave_copy(uint8_t* dst, const uint8_t* src, int32_t len, uint32_t lane) {
+// Progress signal of a long copy (the pipelined decoder's watchdog
+// heartbeat, see wait_for); the one-wave decoder passes none.
+struct NoBeat {
+    LZ4E_DEV void operator()() const {}
+};
+
+template <int kU = 1, class Beat = NoBeat>
+LZ4E_DEV void wave_copy(uint8_t* dst, const uint8_t* src, int32_t len, uint32_t lane,
+                        Beat beat = Beat()) {
     constexpr int32_t kStep = 16 * kWave;
     int32_t k = 16 * (int32_t)lane;
     if constexpr (kU > 1) {
@@ -321,6 +328,7 @@ LZ4E_DEV void wave_copy(uint8_t* dst, const uint8_t* src, int32_t len, uint32_t 
             for (int j = 0; j < kU; ++j) v[j] = *reinterpret_cast<const uint4*>(src + k + j * kStep);
 #pragma unroll
             for (int j = 0; j < kU; ++j) *reinterpret_cast<uint4*>(dst + k + j * kStep) = v[j];
+            beat();
         }
     }
     for (; k + 16 <= len; k += 16 * kWave)
@@ -329,7 +337,9 @@ LZ4E_DEV void wave_copy(uint8_t* dst, const uint8_t* src, int32_t len, uint32_t 
 }
 
 // Whole-wave match copy: out[op + t] = out[op - off + t mod off].
-LZ4E_DEV void wave_match(uint8_t* out, int32_t op, uint32_t off, int32_t len, uint32_t lane) {
+template <class Beat = NoBeat>
+LZ4E_DEV void wave_match(uint8_t* out, int32_t op, uint32_t off, int32_t len, uint32_t lane,
+                         Beat beat = Beat()) {
     if (off == 0) {
         for (int32_t t = lane; t < len; t += kWave) out[op + t] = 0;
         return;
@@ -346,6 +356,7 @@ LZ4E_DEV void wave_match(uint8_t* out, int32_t op, uint32_t off, int32_t len, ui
                 for (int32_t t = k; t < len && t < k + 16; ++t) out[op + t] = out[src + t];
             }
             wave_fence();
+            beat();
         }
         return;
     }
@@ -364,6 +375,7 @@ LZ4E_DEV void wave_match(uint8_t* out, int32_t op, uint32_t off, int32_t len, ui
             for (int32_t t = k; t < len && t < k + 16; ++t) out[op + t] = out[op + t - P];
         }
         wave_fence();
+        beat();
     }
 }
 
@@ -773,9 +785,9 @@ fail:
 // literal run, then the match; same-wave stores and loads to one global
 // address are ordered by the hardware (one vector L1 per CU) and the
 // wavefront fences keep the compiler from moving loads above the stores.
-template <int kU = 1>
+template <int kU = 1, class Beat = NoBeat>
 LZ4E_DEV void copy_scalar_hbm(const Batch& b, const uint8_t* in, int32_t srcSize, uint8_t* gout,
-                              int32_t outSize, uint32_t lane) {
+                              int32_t outSize, uint32_t lane, Beat beat = Beat()) {
     const int32_t L = lane_val((uint32_t)b.L, 0), op = lane_val((uint32_t)b.op, 0);
     const int32_t ls = lane_val((uint32_t)b.ls, 0);
     const int32_t M = lane_val((uint32_t)b.M, 0), off = lane_val((uint32_t)b.off, 0);
@@ -783,14 +795,14 @@ LZ4E_DEV void copy_scalar_hbm(const Batch& b, const uint8_t* in, int32_t srcSize
     if (L > 0 && L <= kLong) {
         if (lane == 0) lane_copy64(gout + op, in + ls, L, in + srcSize);
     } else if (L > kLong) {
-        wave_copy<kU>(gout + op, in + ls, L, lane);
+        wave_copy<kU>(gout + op, in + ls, L, lane, beat);
     }
     wave_fence();
     const int32_t ms = op + L;
     if (M > 0 && M <= kLong) {
         if (lane == 0) lane_match(gout + ms, (uint32_t)off, M, gout + outSize);
     } else if (M > kLong) {
-        wave_match(gout, ms, (uint32_t)off, M, lane);
+        wave_match(gout, ms, (uint32_t)off, M, lane, beat);
     }
     wave_fence();
 }
@@ -1034,11 +1046,21 @@ struct PipeLds {
     int32_t stored;                            // output prefix known to be in HBM
     int32_t nb_total;                          // batches, once the parser is done
     int32_t abort;                             // a wait timed out (watchdog): every wave leaves
+    int32_t beat;                              // heartbeat of a long in-HBM copy (watchdog)
 };
 
-// Watchdog of the waits: a wait that outlasts ~2^23 sleeps (~1 s) means a
-// broken invariant; the block then fails (ret = kPipeAbort) instead of hanging.
-constexpr uint32_t kSpinMax = 1u << 23;
+// Watchdog of the waits: ~2^23 sleeps (~1 s) in a row during which the
+// counter a wait watches does not move means a broken invariant; the block
+// then fails (ret = kPipeAbort = LZ4E_DECODE_ABORTED, include/lz4e.h: the
+// host entry points report it through lz4e_last_error) instead of hanging.
+// Progress resets the count, so a wait behind one long HBM copy (a huge run
+// near LZ4E_MAX_INPUT_SIZE, copied 4 KiB per round trip) never fires it
+// while the copier ahead of it keeps moving its counter.  LZ4E_SPIN_MAX
+// overrides the limit (the emulator's watchdog test builds a small one).
+#ifndef LZ4E_SPIN_MAX
+#define LZ4E_SPIN_MAX (1u << 23)
+#endif
+constexpr uint32_t kSpinMax = LZ4E_SPIN_MAX;
 constexpr int32_t kPipeAbort = INT32_MIN;
 
 LZ4E_DEV int32_t lds_acquire(int32_t* p) {
@@ -1086,10 +1108,18 @@ struct PipeStamps {
     }
 };
 
-// Waits until ready(); false when the watchdog fired (here or in another wave).
-template <class F>
-LZ4E_DEV bool wait_for(PipeLds& S, F ready) {
+// Waits until ready(); false when the watchdog fired (here or in another
+// wave).  watch() is the LDS counter the wait depends on: the watchdog
+// counts sleeps since it last moved.
+template <class F, class W>
+LZ4E_DEV bool wait_for(PipeLds& S, F ready, W watch) {
+    int32_t last = watch();
     for (uint32_t k = 0; !ready(); ++k) {
+        const int32_t now = watch();
+        if (now != last) {
+            last = now;
+            k = 0;
+        }
         if (k >= kSpinMax || lds_acquire(&S.abort)) {
             lds_release(&S.abort, 1);
             return false;
@@ -1099,10 +1129,10 @@ LZ4E_DEV bool wait_for(PipeLds& S, F ready) {
     return true;
 }
 
-template <bool kStamps, class F>
-LZ4E_DEV bool spin(PipeLds& S, F ready, PipeStamps& st, int k) {
+template <bool kStamps, class F, class W>
+LZ4E_DEV bool spin(PipeLds& S, F ready, W watch, PipeStamps& st, int k) {
     st.lap(kStamps, kStWork);
-    const bool ok = wait_for(S, ready);
+    const bool ok = wait_for(S, ready, watch);
     st.lap(kStamps, k);
     return ok;
 }
@@ -1129,7 +1159,8 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
     int32_t nf = 0;
     if (valid && b.off != 0 && ss < F) nf = b.M < F - ss ? b.M : F - ss;
     if (ballot(nf > 0) &&
-        !spin<kStamps>(S, [&] { return lds_acquire(&S.stored) >= F; }, st, kStFar))
+        !spin<kStamps>(S, [&] { return lds_acquire(&S.stored) >= F; },
+                       [&] { return lds_acquire(&S.stored) + lds_acquire(&S.beat); }, st, kStFar))
         return false;
     // loads first (far source bytes, the literal run), consumed below
     uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0, lv = h0;
@@ -1233,7 +1264,9 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
     }
     st.lap(kStamps, kStRounds);
     // cross bytes: batches j-1 and j-2 are final once `resolved` reaches j
-    if (!spin<kStamps>(S, [&] { return lds_acquire(&S.resolved) >= j; }, st, kStPrev)) return false;
+    if (!spin<kStamps>(S, [&] { return lds_acquire(&S.resolved) >= j; },
+                       [&] { return lds_acquire(&S.resolved) + lds_acquire(&S.beat); }, st, kStPrev))
+        return false;
     if (ballot(has_cross)) {
         const int32_t lo1 = hdr[kHdrLo1], lo2 = hdr[kHdrLo2];
         const lu8* p1 = (const lu8*)S.span[(uint32_t)(j + kPipeSpans - 1) % kPipeSpans] - (lo1 & ~15);
@@ -1285,7 +1318,9 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
         }
     }
     st.lap(kStamps, kStSpass);
-    if (!spin<kStamps>(S, [&] { return lds_acquire(&S.stored) >= lo; }, st, kStStore)) return false;
+    if (!spin<kStamps>(S, [&] { return lds_acquire(&S.stored) >= lo; },
+                       [&] { return lds_acquire(&S.stored) + lds_acquire(&S.beat); }, st, kStStore))
+        return false;
     stores_done();
     lds_release(&S.stored, hi);
     st.lap(kStamps, kStVm);
@@ -1318,6 +1353,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
         S.resolved = 0;
         S.stored = 0;
         S.abort = 0;
+        S.beat = 0;
     }
     __syncthreads();
     PipeStamps st;
@@ -1352,7 +1388,8 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
             if (j >= 2 && hbm2) F = F > hi2 ? F : hi2;
             if (j >= 1 && hbm1) F = F > hi1 ? F : hi1;
             const uint32_t slot = (uint32_t)j % kPipeRecs;
-            if (!wait_for(S, [&] { return lds_acquire(&S.con[slot]) == j - (int32_t)kPipeRecs; })) {
+            if (!wait_for(S, [&] { return lds_acquire(&S.con[slot]) == j - (int32_t)kPipeRecs; },
+                          [&] { return lds_acquire(&S.beat) + lds_acquire(&S.con[slot]); })) {
                 if (lane == 0) ret[b] = kPipeAbort;
                 break;
             }
@@ -1391,9 +1428,9 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
         for (int32_t j = (int32_t)c;; j += kCopiers) {
             const uint32_t slot = (uint32_t)j % kPipeRecs;
             st.lap(kStamps, kStWork);
-            const bool ok = wait_for(S, [&] {
-                return lds_acquire(&S.pub[slot]) == j || lds_acquire(&S.nb_total) <= j;
-            });
+            const bool ok = wait_for(
+                S, [&] { return lds_acquire(&S.pub[slot]) == j || lds_acquire(&S.nb_total) <= j; },
+                [&] { return lds_acquire(&S.beat) + lds_acquire(&S.pub[slot]); });
             st.lap(kStamps, kStRec);
             if (!ok) {
                 if (lane == 0) ret[b] = kPipeAbort;
@@ -1414,12 +1451,15 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
             st.bump(kStamps, kStBatches);
             if (hdr[kHdrKind] == kKindHbm) {
                 // every earlier batch in HBM, then in place
-                if (!spin<kStamps>(S, [&] { return lds_acquire(&S.stored) >= hdr[kHdrLo]; }, st,
-                                   kStStore)) {
+                if (!spin<kStamps>(S, [&] { return lds_acquire(&S.stored) >= hdr[kHdrLo]; },
+                                   [&] { return lds_acquire(&S.stored) + lds_acquire(&S.beat); }, st, kStStore)) {
                     if (lane == 0) ret[b] = kPipeAbort;
                     break;
                 }
-                copy_scalar_hbm<4>(bt, in, srcSize, gout, outSize, lane);
+                copy_scalar_hbm<4>(bt, in, srcSize, gout, outSize, lane, [&] {
+                    const int32_t v = lds_acquire(&S.beat);
+                    if (lane == 0) lds_release(&S.beat, v + 1);
+                });
                 stores_done();
                 lds_release(&S.resolved, j + 1);
                 lds_release(&S.stored, hdr[kHdrHi]);

@@ -529,14 +529,20 @@ int decompress_batch_impl(const char* const* src, const int* csize, char* const*
     }
     if (!ok) return -1;
     int good = 0;
+    bool aborted = false;
     for (uint32_t i = 0; i < R; ++i) {
         ret[i] = reinterpret_cast<const int32_t*>(hd + m_rt)[i];
+        if (ret[i] == LZ4E_DECODE_ABORTED && !aborted) {
+            aborted = true;
+            set_err("lz4e: decoder watchdog fired on block " + std::to_string(i) +
+                    " (a wait made no progress; LZ4E_DECODE_ABORTED)");
+        }
         if (ret[i] >= 0) {
             if (ret[i] > 0) std::memcpy(dst[i], hd + dso[i], (size_t)ret[i]);
             good++;
         }
     }
-    return good;
+    return aborted ? -1 : good;
 }
 
 }  // namespace
@@ -647,14 +653,22 @@ int lz4e_debug_decompress_stamped(const uint8_t* src, const uint64_t* src_off, c
                : -1;
 }
 
-int lz4e_decompress_batch_dev(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
-                              uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
-                              int32_t* ret, uint32_t nblocks, uint32_t max_cap, void* stream) {
+int lz4e_decompress_batch_dev2(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
+                               uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
+                               int32_t* ret, uint32_t nblocks, uint32_t max_cap, void* stream) {
     g_err.clear();
     lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap};
     return hip_ok(lz4e::launch_decompress(a, static_cast<hipStream_t>(stream)), "decompress launch")
                ? 0
                : -1;
+}
+
+// The round-1 signature (no max_cap: the pipelined decoder for every block).
+int lz4e_decompress_batch_dev(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
+                              uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
+                              int32_t* ret, uint32_t nblocks, void* stream) {
+    return lz4e_decompress_batch_dev2(src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, 0,
+                                      stream);
 }
 
 int lz4e_compress_batch_dev_dict(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
@@ -833,6 +847,12 @@ bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chu
     const int32_t* ret = reinterpret_cast<const int32_t*>(hm + s.meta_ret);
     const int32_t* dret = reinterpret_cast<const int32_t*>(hm + s.meta_dret);
     const uint32_t R = (uint32_t)s.req.size();
+    for (uint32_t j = 0; j < R; ++j) {
+        if (dret[j] == LZ4E_DECODE_ABORTED) {
+            set_err("lz4e: decoder watchdog fired (a wait made no progress; LZ4E_DECODE_ABORTED)");
+            return false;
+        }
+    }
     par_for(R, s.out_bytes, [&](uint32_t j) {
         lz4e_chunk_request& q = reqs[s.req[j]];
         const int32_t len = (int32_t)q.srcIter->bi_size;
@@ -852,16 +872,20 @@ bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chu
         q.status = 0;
     });
     if (pr.on) pr.out += now_ms() - t1;
+    // Stats as the reference keeps them: lz4e_stats_update runs only in
+    // lz4e_end_io (lz4e_bdev/lz4e_req.c:231-246), i.e. for a WRITE whose
+    // round trip succeeded and whose bio was submitted; a request failing in
+    // lz4e_write_req_init (compress or decompress failure, -EIO) returns
+    // through lz4e_dev.c:187-202 without touching any counter.  reqs_failed
+    // counts completed bios the underlying device failed (lz4e_stats.c:43-45):
+    // there is no underlying device here, so it stays 0.
     for (uint32_t j = 0; j < R; ++j) {
         const lz4e_chunk_request& q = reqs[s.req[j]];
-        if (q.status == 0) good++;
+        if (q.status != 0) continue;
+        good++;
         st.reqs_total++;
-        if (q.status != 0) {
-            st.reqs_failed++;
-        } else {
-            st.data_in_bytes += q.srcIter->bi_size;
-            st.vec_count += bio_vcnt_of_buffer(q.data, q.srcIter->bi_size);
-        }
+        st.data_in_bytes += q.srcIter->bi_size;
+        st.vec_count += bio_vcnt_of_buffer(q.data, q.srcIter->bi_size);
         st.frame_bytes += (uint64_t)q.comp_size;
     }
     s.req.clear();
@@ -951,14 +975,9 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
             const lz4e_chunk_request& q = reqs[i];
             const uint32_t len = q.srcIter->bi_size;
             int t = LZ4E_TABLE_BYU16;
-            if (len > LZ4E_MAX_INPUT_SIZE) {  // lz4e_compress.c:245-248 -> -EIO
-                st.reqs_total++, st.reqs_failed++;
-                continue;
-            }
-            if (len >= 13 && (t = table_type_of(q.src, q.srcIter)) == 0) {  // :274-277
-                st.reqs_total++, st.reqs_failed++;
-                continue;
-            }
+            // compress returns 0 -> -EIO, no stats (lz4e_dev.c:187-202)
+            if (len > LZ4E_MAX_INPUT_SIZE) continue;  // lz4e_compress.c:245-248
+            if (len >= 13 && (t = table_type_of(q.src, q.srcIter)) == 0) continue;  // :274-277
             s.req.push_back(i);
             in.push_back(ib);
             tt.push_back((uint8_t)t);

@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = (
     "LZ4E_compress_default", "LZ4E_decompress_safe", "lz4e_sg_table_type",
     "lz4e_last_error", "lz4e_gpu_available", "lz4e_compress_sg_batch",
     "lz4e_decompress_batch", "lz4e_compress_batch_dev", "lz4e_decompress_batch_dev",
+    "lz4e_decompress_batch_dev2",
     "lz4e_chunk_write_batch", "lz4e_decompress_safe_sg", "lz4e_decompress_sg_batch",
     "LZ4E_compress_usingDict", "LZ4E_decompress_safe_usingDict", "lz4e_compress_sg_batch_dict",
     "lz4e_decompress_batch_dict", "lz4e_compress_batch_dev_dict", "lz4e_decompress_batch_dev_dict",
@@ -134,8 +135,10 @@ def lib() -> ctypes.CDLL:
     L.lz4e_decompress_batch.restype = I32
     L.lz4e_compress_batch_dev.argtypes = [P, P, P, P, P, P, P, P, P, U32, U32, P]
     L.lz4e_compress_batch_dev.restype = I32
-    L.lz4e_decompress_batch_dev.argtypes = [P, P, P, P, P, P, P, U32, U32, P]
+    L.lz4e_decompress_batch_dev.argtypes = [P, P, P, P, P, P, P, U32, P]
     L.lz4e_decompress_batch_dev.restype = I32
+    L.lz4e_decompress_batch_dev2.argtypes = [P, P, P, P, P, P, P, U32, U32, P]
+    L.lz4e_decompress_batch_dev2.restype = I32
     L.lz4e_chunk_write_batch.argtypes = [ctypes.POINTER(ChunkRequest), I32, ctypes.POINTER(ChunkStats)]
     L.lz4e_chunk_write_batch.restype = I32
     L.lz4e_decompress_safe_sg.argtypes = [P, ctypes.POINTER(BioVec), ctypes.POINTER(BvecIter), I32]
@@ -501,7 +504,7 @@ def compress_batch_dev(src, src_off, src_len, table_type_, dst, dst_off, dst_cap
 
 def decompress_batch_dev(src, src_off, src_len, dst, dst_off, dst_cap, ret, stream=None,
                          max_cap: Optional[int] = None) -> None:
-    """lz4e_decompress_batch_dev on torch tensors (launch only).
+    """lz4e_decompress_batch_dev2 on torch tensors (launch only).
 
     ``max_cap`` bounds dst_cap (default: read from it, which synchronises);
     16 KiB and more selects the pipelined 4-wave decoder, smaller blocks
@@ -515,8 +518,8 @@ def decompress_batch_dev(src, src_off, src_len, dst, dst_off, dst_cap, ret, stre
                dst_cap=dst_cap, ret=ret)
     if stream is None:
         stream = torch.cuda.current_stream().cuda_stream
-    r = lib().lz4e_decompress_batch_dev(_ptr(src), _ptr(src_off), _ptr(src_len), _ptr(dst),
-                                        _ptr(dst_off), _ptr(dst_cap), _ptr(ret), n,
-                                        max(0, int(max_cap)), stream)
+    r = lib().lz4e_decompress_batch_dev2(_ptr(src), _ptr(src_off), _ptr(src_len), _ptr(dst),
+                                         _ptr(dst_off), _ptr(dst_cap), _ptr(ret), n,
+                                         max(0, int(max_cap)), stream)
     if r != 0:
-        raise RuntimeError("lz4e_decompress_batch_dev: " + last_error())
+        raise RuntimeError("lz4e_decompress_batch_dev2: " + last_error())

@@ -85,6 +85,12 @@ def rebalance_plan(queues: Sequence[Sequence[int]], chunk_blocks: Sequence[int],
     projected time moves to the rank with the smallest one, as long as that
     lowers the larger of the two projected times.  Deterministic: every rank
     computes the same plan from the same all_gathered numbers.
+
+    A chunk moves at most once: a received chunk is appended to its new
+    rank's queue but never given away again (the payload exchange is one
+    batch of point-to-point transfers, so a chunk relayed through a middle
+    rank would be forwarded before it had arrived).  The chunk taken from the
+    most loaded rank is the last one it held from the start.
     """
     world = len(queues)
     q = [list(x) for x in queues]
@@ -99,19 +105,24 @@ def rebalance_plan(queues: Sequence[Sequence[int]], chunk_blocks: Sequence[int],
     rate = [x if x else fallback for x in rate]
     proj = [blocks[r] / rate[r] for r in range(world)]
     moves: List[Tuple[int, int, int]] = []
+    moved = set()
     while len(moves) < max_moves:
         hi = max(range(world), key=lambda r: (proj[r], -r))
         lo = min(range(world), key=lambda r: (proj[r], r))
-        if hi == lo or not q[hi]:
+        if hi == lo:
             break
-        c = q[hi][-1]
+        own = [i for i, x in enumerate(q[hi]) if x not in moved]
+        if not own:
+            break
+        c = q[hi][own[-1]]
         nb = chunk_blocks[c]
         new_hi = proj[hi] - nb / rate[hi]
         new_lo = proj[lo] + nb / rate[lo]
         if max(new_hi, new_lo) >= proj[hi]:
             break
-        q[hi].pop()
+        del q[hi][own[-1]]
         q[lo].append(c)
+        moved.add(c)
         proj[hi], proj[lo] = new_hi, new_lo
         moves.append((c, hi, lo))
     return moves

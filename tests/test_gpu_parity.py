@@ -388,7 +388,9 @@ def _chunk_check(gpu, srcs, payloads, want_frames=True):
         if want_frames:
             assert frame == ef
     assert good == len(srcs) - nfail
-    assert stats.reqs_total == len(srcs) and stats.reqs_failed == nfail
+    # only completed round trips count (lz4e_end_io, lz4e_req.c:231-246); a
+    # request failing in lz4e_write_req_init touches no counter (lz4e_dev.c:187-202)
+    assert stats.reqs_total == len(srcs) - nfail and stats.reqs_failed == 0
     # one merged bio_vec per successful non-empty request (lz4e_stats.c:47)
     assert stats.vec_count == sum(1 for s, b in zip(srcs, payloads) if gpu.table_type(s) and len(b))
     assert stats.data_in_bytes == sum(len(b) for s, b in zip(srcs, payloads) if gpu.table_type(s))

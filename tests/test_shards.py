@@ -198,3 +198,110 @@ def test_bench_launches_ranks():
     bad = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--dry-run"],
                          capture_output=True, text=True, timeout=60, env=env)
     assert bad.returncode != 0 and "WORLD_SIZE" in bad.stderr
+
+
+def test_rebalance_plan_moves_each_chunk_once():
+    """3, 4 and 8 ranks, uneven busy times: no chunk appears twice in a plan
+    (a chunk relayed through a middle rank would be forwarded, in the same
+    batch of point-to-point transfers, before it had arrived: ADVICE r02),
+    the plan is a permutation of the chunks, and it never raises the
+    projected slowest rank."""
+    import random
+    rng = random.Random(20260517)
+    for _ in range(4000):
+        world = rng.choice([3, 4, 8])
+        n = rng.randint(world, 96)
+        queues = deal_chunks(n, world)
+        nb = [16] * n
+        nb[-1] = rng.randint(1, 16)
+        busy = [rng.uniform(0.5, 2.0) * sum(nb[c] for c in q) for q in queues]
+        moves = rebalance_plan(queues, nb, busy)
+        moved = [c for c, _, _ in moves]
+        assert len(moved) == len(set(moved))
+        q2 = apply_moves(queues, moves)
+        assert sorted(sum(q2, [])) == list(range(n))
+        rate = [sum(nb[c] for c in q) / b for q, b in zip(queues, busy)]
+        proj = lambda qs: max(sum(nb[c] for c in q) / r for q, r in zip(qs, rate))
+        assert proj(q2) <= proj(queues) + 1e-12
+        # every move leaves its chunk's original owner
+        assert all(c in queues[a] for c, a, _ in moves)
+
+
+def _strong_worker(rank, world, port, n_blocks, chunk, out_dir):
+    """The calls bench.strong_scaling makes, in its order (ChunkQueue ->
+    progress -> rebalance -> rebuild from the held chunks), with the
+    calibration busy time measured: the oracle compressing this rank's
+    chunks.  Rank 0's blocks are text (slow to compress), rank 1's are
+    incompressible bytes (the search skips ahead): two block classes."""
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import oracle_ref
+    bs = 4096
+    q = ChunkQueue(n_blocks, chunk, rank, world)
+    text = corpus.text_proxy(n_blocks * bs, 11)
+    rnd = np.random.default_rng(12).integers(0, 256, n_blocks * bs, dtype=np.uint8)
+    owner0 = set(deal_chunks(q.n_chunks, world)[0])
+
+    def payload(c):
+        lo, hi = q.chunk_range(c)
+        src = text if c in owner0 else rnd
+        return torch.from_numpy(src[lo * bs:hi * bs].copy())
+
+    held = {c: payload(c) for c in q.queue}
+    t0 = time.perf_counter()
+    for _ in range(3):
+        for c in q.queue:
+            buf = held[c].numpy()
+            for k in range(len(buf) // bs):
+                oracle_ref.compress(buf[k * bs:(k + 1) * bs].tobytes(), BYU16)
+    busy = time.perf_counter() - t0
+    stats = q.progress(len(q.blocks()), 0, busy, dist.group.WORLD)
+    moves = q.rebalance(stats, held, lambda c: (q.chunk_range(c)[1] - q.chunk_range(c)[0]) * bs,
+                        dist.group.WORLD)
+    assert sorted(held) == sorted(q.queue)
+    out = {}
+    for c in q.queue:
+        assert torch.equal(held[c], payload(c))  # every received payload is the chunk's bytes
+        lo, hi = q.chunk_range(c)
+        buf = held[c].numpy()
+        for k, blk in enumerate(range(lo, hi)):
+            out[blk] = oracle_ref.compress(buf[k * bs:(k + 1) * bs].tobytes(), BYU16)[1]
+    with open(os.path.join(out_dir, f"s{rank}.txt"), "w") as f:
+        f.write(" ".join(f"{x:.6f}" for _, _, x in stats) + "\n")
+        f.write(" ".join(f"{c},{a},{b}" for c, a, b in moves) + "\n")
+        f.write(" ".join(f"{b}:{out[b].hex()}" for b in sorted(out)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_strong_scaling_calls(tmp_path):
+    """ChunkQueue through bench.strong_scaling's calls with measured
+    calibration of two block classes: the plan is the same on both ranks,
+    moves chunks only off the slower (text) rank, and the job's frames
+    equal the single-process ones."""
+    import oracle_ref
+    world, n, chunk = 2, 48, 4
+    mp.spawn(_strong_worker, args=(world, _free_port(), n, chunk, str(tmp_path)), nprocs=world,
+             join=True)
+    lines = [open(tmp_path / f"s{r}.txt").read().split("\n") for r in range(world)]
+    assert lines[0][0] == lines[1][0] and lines[0][1] == lines[1][1]
+    busy = [float(x) for x in lines[0][0].split()]
+    assert busy[0] > busy[1]  # text compresses slower than incompressible bytes
+    moves = [tuple(map(int, m.split(","))) for m in lines[0][1].split()]
+    assert moves and all(a == 0 and b == 1 for _, a, b in moves)
+    frames = {}
+    for r in range(world):
+        for tok in lines[r][2].split():
+            b, h = tok.split(":")
+            assert int(b) not in frames
+            frames[int(b)] = bytes.fromhex(h)
+    assert sorted(frames) == list(range(n))
+    bs = 4096
+    text = corpus.text_proxy(n * bs, 11)
+    rnd = np.random.default_rng(12).integers(0, 256, n * bs, dtype=np.uint8)
+    owner0 = set(deal_chunks(-(-n // chunk), world)[0])
+    for b in range(n):
+        src = text if b // chunk in owner0 else rnd
+        assert frames[b] == oracle_ref.compress(src[b * bs:(b + 1) * bs].tobytes(), BYU16)[1]
