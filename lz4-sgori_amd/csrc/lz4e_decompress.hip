@@ -43,6 +43,7 @@
 #include "lz4e_device.h"
 #include "lz4e_gpu.h"
 #include "lz4e_order.h"
+#include "lz4e_results.h"
 
 namespace lz4e {
 
@@ -1047,6 +1048,7 @@ struct PipeLds {
     int32_t nb_total;                          // batches, once the parser is done
     int32_t abort;                             // a wait timed out (watchdog): every wave leaves
     int32_t beat;                              // heartbeat of a long in-HBM copy (watchdog)
+    int32_t result;                            // the parse's return value (decided by wave 0)
 };
 
 // Watchdog of the waits: ~2^23 sleeps (~1 s) in a row during which the
@@ -1061,12 +1063,15 @@ struct PipeLds {
 #define LZ4E_SPIN_MAX (1u << 23)
 #endif
 constexpr uint32_t kSpinMax = LZ4E_SPIN_MAX;
-constexpr int32_t kPipeAbort = INT32_MIN;
+constexpr int32_t kPipeAbort = kDecodeAborted;  // lz4e_results.h
 
 LZ4E_DEV int32_t lds_acquire(int32_t* p) {
     return (int32_t)uni((uint32_t)__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
 }
+// Called by every lane of the wave: the wave's earlier LDS / global
+// accesses have all been issued before it (lockstep).
 LZ4E_DEV void lds_release(int32_t* p, int32_t v) {
+    lockstep();
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -1354,6 +1359,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
         S.stored = 0;
         S.abort = 0;
         S.beat = 0;
+        S.result = kPipeAbort;
     }
     __syncthreads();
     PipeStamps st;
@@ -1380,7 +1386,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
             });
             st.lap(kStamps, kStParse);
             if (pr == kParseFail) {
-                if (lane == 0) ret[b] = -P.ip - 1;
+                if (lane == 0) S.result = -P.ip - 1;
                 break;
             }
             // far line: sources before it are read from HBM (see copy_fast)
@@ -1390,7 +1396,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
             const uint32_t slot = (uint32_t)j % kPipeRecs;
             if (!wait_for(S, [&] { return lds_acquire(&S.con[slot]) == j - (int32_t)kPipeRecs; },
                           [&] { return lds_acquire(&S.beat) + lds_acquire(&S.con[slot]); })) {
-                if (lane == 0) ret[b] = kPipeAbort;
+                lds_release(&S.abort, 1);
                 break;
             }
             st.lap(kStamps, kStPWait);
@@ -1416,7 +1422,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
             hbm1 = pr == kParsedScalar;
             j++;
             if (P.done) {
-                if (lane == 0) ret[b] = P.op;
+                if (lane == 0) S.result = P.op;
                 break;
             }
         }
@@ -1433,7 +1439,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
                 [&] { return lds_acquire(&S.beat) + lds_acquire(&S.pub[slot]); });
             st.lap(kStamps, kStRec);
             if (!ok) {
-                if (lane == 0) ret[b] = kPipeAbort;
+                lds_release(&S.abort, 1);
                 break;
             }
             if (lds_acquire(&S.pub[slot]) != j) break;  // the parser ended before batch j
@@ -1453,23 +1459,32 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
                 // every earlier batch in HBM, then in place
                 if (!spin<kStamps>(S, [&] { return lds_acquire(&S.stored) >= hdr[kHdrLo]; },
                                    [&] { return lds_acquire(&S.stored) + lds_acquire(&S.beat); }, st, kStStore)) {
-                    if (lane == 0) ret[b] = kPipeAbort;
+                    lds_release(&S.abort, 1);
                     break;
                 }
                 copy_scalar_hbm<4>(bt, in, srcSize, gout, outSize, lane, [&] {
-                    const int32_t v = lds_acquire(&S.beat);
-                    if (lane == 0) lds_release(&S.beat, v + 1);
+                    // (called in lane-divergent loops: lane 0 alone, no ordering)
+                    if (lane == 0)
+                        __hip_atomic_fetch_add(&S.beat, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 });
                 stores_done();
                 lds_release(&S.resolved, j + 1);
                 lds_release(&S.stored, hdr[kHdrHi]);
                 st.lap(kStamps, kStVm);
             } else if (!copy_fast<kStamps>(S, c, j, bt, hdr, in, srcSize, gout, lane, st)) {
-                if (lane == 0) ret[b] = kPipeAbort;
+                lds_release(&S.abort, 1);
                 break;
             }
         }
     }
+    // Every wave has left its loop (each wait is bounded by the watchdog):
+    // the block's value is the parse's unless a wave gave up, which fails
+    // the whole block -- the parser may finish its parse without ever
+    // waiting, so only here are all waves' outcomes known.
+    __syncthreads();
+    if (tid == 0) ret[b] = __hip_atomic_load(&S.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                               ? kPipeAbort
+                               : S.result;
     if constexpr (kStamps) {
         if (lane == 0 && dbg) {
             uint64_t* d = dbg + kStSlots * (size_t)b;

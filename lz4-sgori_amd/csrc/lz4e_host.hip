@@ -27,6 +27,9 @@
 
 #include "../../include/lz4e.h"
 #include "lz4e_gpu.h"
+#include "lz4e_results.h"
+
+static_assert(lz4e::kDecodeAborted == LZ4E_DECODE_ABORTED, "watchdog return value");
 
 namespace {
 
@@ -528,21 +531,16 @@ int decompress_batch_impl(const char* const* src, const int* csize, char* const*
              hip_ok(hipStreamSynchronize(c.stream), "decompress sync");
     }
     if (!ok) return -1;
-    int good = 0;
-    bool aborted = false;
-    for (uint32_t i = 0; i < R; ++i) {
-        ret[i] = reinterpret_cast<const int32_t*>(hd + m_rt)[i];
-        if (ret[i] == LZ4E_DECODE_ABORTED && !aborted) {
-            aborted = true;
-            set_err("lz4e: decoder watchdog fired on block " + std::to_string(i) +
-                    " (a wait made no progress; LZ4E_DECODE_ABORTED)");
-        }
-        if (ret[i] >= 0) {
-            if (ret[i] > 0) std::memcpy(dst[i], hd + dso[i], (size_t)ret[i]);
-            good++;
-        }
+    for (uint32_t i = 0; i < R; ++i) ret[i] = reinterpret_cast<const int32_t*>(hd + m_rt)[i];
+    std::string err;
+    const int good = lz4e::decode_results(ret, R, err);
+    if (good < 0) {
+        set_err(err);
+        return -1;
     }
-    return aborted ? -1 : good;
+    for (uint32_t i = 0; i < R; ++i)
+        if (ret[i] > 0) std::memcpy(dst[i], hd + dso[i], (size_t)ret[i]);
+    return good;
 }
 
 }  // namespace
@@ -847,9 +845,10 @@ bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chu
     const int32_t* ret = reinterpret_cast<const int32_t*>(hm + s.meta_ret);
     const int32_t* dret = reinterpret_cast<const int32_t*>(hm + s.meta_dret);
     const uint32_t R = (uint32_t)s.req.size();
-    for (uint32_t j = 0; j < R; ++j) {
-        if (dret[j] == LZ4E_DECODE_ABORTED) {
-            set_err("lz4e: decoder watchdog fired (a wait made no progress; LZ4E_DECODE_ABORTED)");
+    {
+        std::string err;
+        if (lz4e::decode_results(dret, R, err) < 0) {
+            set_err(err);
             return false;
         }
     }

@@ -1,9 +1,17 @@
 // lz4e_wave.h -- the wave64 primitives the gfx950 LZ4E kernels are written
 // against: lane identity, ballots, cross-lane reads, byte alignment, the
 // shader clock and the global-memory pointer types.  Kernel code uses only
-// these (never the amdgcn builtins directly), so the whole parse can also be
-// exercised lane-by-lane by the host-side emulator under tools/emu/, which
-// supplies its own version of this one header.
+// these (never the amdgcn builtins directly).
+//
+// The host-side lane emulator (tools/emu/, test tooling) compiles this same
+// header: it supplies the amdgcn builtins themselves (each lane a thread,
+// tools/emu/include/hip/hip_runtime.h, with the hardware's semantics: DPP row
+// shifts and broadcasts, ds_(b)permute, v_perm, ...), so every helper below
+// -- match_any6, the DPP scans, the byte-table gathers -- runs the same code
+// there.  Only what a host thread cannot express differs under LZ4E_EMU:
+// inline asm (register constraints, m0), the buffer-resource type, and the
+// places that rely on a wave's lanes running in lockstep, which become
+// barriers of the emulated wave.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -29,6 +37,7 @@ LZ4E_DEV uint32_t set_lane(uint32_t v, uint32_t x, uint32_t l) {
 // builtin exists; gfx9 takes a variable lane select from m0 only (as the
 // compiler's own lowering of llvm.amdgcn.writelane does, m0 being set right
 // before every use), and the s_nop covers the lane-select hazard.
+#ifndef LZ4E_EMU
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
 LZ4E_DEV uint32_t put_lane(uint32_t v, uint32_t x, uint32_t l) {
@@ -39,6 +48,11 @@ LZ4E_DEV uint32_t put_lane(uint32_t v, uint32_t x, uint32_t l) {
     return v;
 }
 #pragma clang diagnostic pop
+#else
+LZ4E_DEV uint32_t put_lane(uint32_t v, uint32_t x, uint32_t l) {
+    return set_lane(v, uni(x), l);
+}
+#endif
 // Lanes whose 6-bit key equals mine (key < 64): one ballot per key bit, no
 // loop over the distinct keys.
 LZ4E_DEV uint64_t match_any6(uint32_t key) {
@@ -67,7 +81,11 @@ LZ4E_DEV uint32_t push_lane(uint32_t v, uint32_t dst) {
 }
 // Keeps a value (e.g. a prefetch load's result) alive until here without
 // using it: the wait for it is placed here, not at the load.
+#ifndef LZ4E_EMU
 LZ4E_DEV void consume(uint32_t v) { asm volatile("" ::"v"(v)); }
+#else
+LZ4E_DEV void consume(uint32_t) {}
+#endif
 // ds_bpermute: lane src's value (src mod 64), per lane.  (HIP's __shfl adds
 // the lane id and a width mask around it: two VALU more per shuffle.)
 LZ4E_DEV uint32_t shfl(uint32_t v, uint32_t src) {
@@ -134,6 +152,7 @@ LZ4E_DEV uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
 }
 // s_memtime: shader clock (diagnostic builds only).
 LZ4E_DEV uint64_t clock64() { return __builtin_amdgcn_s_memtime(); }
+#ifndef LZ4E_EMU
 // Order this wave's LDS/global accesses (memory model fence, wavefront scope).
 LZ4E_DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 // The lanes of a wave execute in lockstep: a memory instruction completes
@@ -142,11 +161,10 @@ LZ4E_DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront
 // followed by a read-back, a lane's store overwriting bytes another lane
 // stored just before -- and emits no code.
 LZ4E_DEV void lockstep() {}
-// Workgroup barrier (one wave per workgroup: orders the LDS staging).
+// Workgroup barrier.
 LZ4E_DEV void block_sync() { __syncthreads(); }
 // Every global store of this wave has completed (before a flag says so).
 LZ4E_DEV void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
 // Moves a (possibly wave-uniform) byte offset into a VGPR.  A uniform load
 // from read-only memory would otherwise become s_load_*, which ignores the
 // low two address bits -- wrong for unaligned reads.
@@ -154,6 +172,16 @@ LZ4E_DEV uint32_t vaddr(uint32_t q) {
     asm("" : "+v"(q));
     return q;
 }
+#else
+// Lane emulator: each lane is a host thread, so every place that relies on
+// lockstep execution is a barrier of the emulated wave; the workgroup
+// barrier is the emulated workgroup's.
+LZ4E_DEV void wave_fence() { emu_wave_barrier(); }
+LZ4E_DEV void lockstep() { emu_wave_barrier(); }
+LZ4E_DEV void block_sync() { __syncthreads(); }
+LZ4E_DEV void stores_done() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }
+LZ4E_DEV uint32_t vaddr(uint32_t q) { return q; }
+#endif
 
 // Global-memory pointer types: pointers rebuilt from integer addresses lose
 // their address space and would otherwise compile to flat_* accesses, which
@@ -162,6 +190,7 @@ typedef __attribute__((address_space(1))) const uint32_t gcu32;
 
 // n bytes at p as a raw buffer resource: dword loads at byte offset q return
 // 0 when the dword is not entirely inside [0, n) (hardware range check).
+#ifndef LZ4E_EMU
 struct ByteBuf {
     __amdgpu_buffer_rsrc_t r;
 };
@@ -172,6 +201,19 @@ LZ4E_DEV ByteBuf buf_make(const void* p, uint32_t n) {
 LZ4E_DEV uint32_t buf_ld32(const ByteBuf& b, uint32_t q) {
     return __builtin_amdgcn_raw_buffer_load_b32(b.r, q, 0, 0);
 }
+#else
+struct ByteBuf {
+    const uint8_t* p;
+    uint32_t n;
+};
+inline ByteBuf buf_make(const void* p, uint32_t n) { return ByteBuf{(const uint8_t*)p, n}; }
+inline uint32_t buf_ld32(const ByteBuf& b, uint32_t q) {
+    if ((uint64_t)q + 4 > b.n) return 0;
+    uint32_t v;
+    __builtin_memcpy(&v, b.p + q, 4);
+    return v;
+}
+#endif
 typedef __attribute__((address_space(1))) const uint8_t gcu8;
 
 }  // namespace lz4e

@@ -1,10 +1,15 @@
-"""The compress kernel's own source on the CPU, under ASan + UBSan.
+"""The kernels' own sources on the CPU, under ASan + UBSan.
 
-tools/emu compiles lz4-sgori_amd/csrc/lz4e_compress.hip unmodified as host
-C++ with every lane of the wave a thread (tools/emu/lz4e_wave.h stands in for
-the wave primitives).  It is the only CPU build of the kernel, so it is where
-out-of-bounds window / candidate / stripe reads get caught before they reach
-a GPU.  Each block's frame and iterator post-state must equal the oracle's.
+tools/emu compiles lz4-sgori_amd/csrc/lz4e_compress.hip and
+lz4e_decompress.hip unmodified as host C++ with every lane a thread, together
+with the product's own csrc/lz4e_wave.h (built with -DLZ4E_EMU; the amdgcn
+builtins it uses -- DPP row shifts, ds_(b)permute, v_perm, ballots -- are
+emulated in tools/emu/include/hip/hip_runtime.h).  Workgroups of several
+waves run as 64 threads per wave: the pipelined decoder's parser and copiers
+meet through its LDS counters as host atomics.  It is the only CPU build of
+the kernels, so it is where out-of-bounds reads and writes get caught before
+they reach a GPU.  Each block's frame and iterator post-state, and each
+decode's value and bytes, must equal the oracle's.
 
 UBSan's alignment check is off: the kernel's unaligned dword loads are legal
 on gfx950 (global loads need no alignment) and are emulated as plain loads.
@@ -220,3 +225,78 @@ def test_emulated_decoder_vector_extension_truncated_in_run(emu_exe_vecext, tmp_
     want = oracle_ref.decompress_dict(ff, 100000, b"")
     got = _emu_decode(emu_exe_vecext, tmp_path, ff, 100000)
     assert got[0] == want[0], (got[0], want[0])
+
+
+# ---------------------------------------------------------------------------
+# The pipelined decoder (decompress_pipe_kernel: one parser wave and three
+# copier waves per block, LDS record ring, spans, progress counters as host
+# atomics) on the emulator, under the same sanitizers.
+# ---------------------------------------------------------------------------
+
+def _emu_decode_pipe(exe, tmp_path, frame, cap, dic=b""):
+    f, o, d = tmp_path / "f.bin", tmp_path / "o.bin", tmp_path / "d.bin"
+    f.write_bytes(frame)
+    d.write_bytes(dic)
+    if o.exists():
+        o.unlink()
+    out = subprocess.run([exe, "-p", str(f), str(cap), str(o), str(d)], capture_output=True, text=True,
+                         timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "ERROR: AddressSanitizer" not in out.stderr and "runtime error" not in out.stderr
+    lines = out.stdout.split("\n")
+    r = int(lines[0].split()[1])
+    return r, (o.read_bytes() if r > 0 else b""), lines[1]
+
+
+PIPE_CASES = [(k, m) for k in ("text", "records", "ints", "runs") for m in range(5)] + [("random", 0)]
+
+
+@pytest.mark.parametrize("kind,mode", PIPE_CASES, ids=[f"{k}-{m}" for k, m in PIPE_CASES])
+def test_emulated_pipe_decoder_sanitized(emu_exe, tmp_path, kind, mode):
+    """The 4-wave pipelined decoder on 16-64 KiB blocks: valid frames (mode
+    0), truncations (1), bit flips (2), short capacity (3) and a dictionary
+    (4): values, error codes and bytes equal the oracle's
+    (/root/reference/lz4e/lz4e_decompress.c:62-460 restated)."""
+    rng = np.random.default_rng(700 + mode + 17 * len(kind))
+    n = int(rng.integers(16384, 65536))
+    data = _block(kind, n + 9000, 31 + n).tobytes()
+    dic, blk = (data[:9000], data[9000:]) if mode == 4 else (b"", data[:n])
+    f = oracle_ref.compress_dict(blk, dic)[1] if mode == 4 else oracle_ref.compress(blk, BYU16)[1]
+    cap = len(blk)
+    if mode == 1:
+        f = f[:int(rng.integers(1, len(f)))]
+    elif mode == 2:
+        fb = bytearray(f)
+        for _ in range(3):
+            fb[int(rng.integers(0, len(fb)))] ^= 1 << int(rng.integers(0, 8))
+        f = bytes(fb)
+    elif mode == 3:
+        cap = max(0, cap - int(rng.integers(1, 40)))
+    want = oracle_ref.decompress_dict(f, cap, dic)
+    got = _emu_decode_pipe(emu_exe, tmp_path, f, cap, dic)
+    assert got[0] == want[0], (got[0], want[0])
+    if want[0] >= 0:
+        assert got[1] == want[1]
+
+
+@pytest.fixture(scope="session")
+def emu_exe_spin1(tmp_path_factory):
+    """The decoders built with a watchdog limit of one sleep: any wait that
+    needs a second poll gives up (LZ4E_SPIN_MAX=1)."""
+    b, exe = _build_emu(tmp_path_factory, "-DLZ4E_SPIN_MAX=1")
+    yield exe
+    shutil.rmtree(b, ignore_errors=True)
+
+
+def test_emulated_pipe_decoder_watchdog(emu_exe_spin1, tmp_path):
+    """A forced watchdog: every wave leaves its loop (the run ends), the
+    block's value is LZ4E_DECODE_ABORTED -- even though the parser itself
+    finished the parse -- and the host's reading of the batch
+    (csrc/lz4e_results.h, used by every host entry point) fails the call
+    with the watchdog named in lz4e_last_error's text."""
+    blk = _block("text", 65536, 9).tobytes()
+    f = oracle_ref.compress(blk, BYU16)[1]
+    r, _, res = _emu_decode_pipe(emu_exe_spin1, tmp_path, f, len(blk))
+    assert r == -2**31
+    good, msg = res.split(" ", 2)[1:]
+    assert int(good) == -1 and "watchdog" in msg and "LZ4E_DECODE_ABORTED" in msg

@@ -1,8 +1,9 @@
 // Lane emulator of the LZ4E compress kernel (debug/test tooling, tools/emu):
-// compiles the unmodified kernel source (copied next to the emulated
-// lz4e_wave.h by build.sh) as host C++ and runs each block as 64 threads.
+// compiles the unmodified kernel source (and csrc/lz4e_wave.h, with
+// -DLZ4E_EMU) as host C++ and runs each workgroup as 64 threads per wave.
 #include <stdint.h>
 #include <string.h>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -21,25 +22,29 @@ namespace lz4e {
 int launch_order_mode(bool) { return kOrderNever; }
 }  // namespace lz4e
 
+thread_local EmuWave* g_emu_wave;
+thread_local uint32_t g_emu_lane;
+thread_local std::barrier<>* g_emu_group;
 dim3 blockIdx;
-namespace lz4e {
-EmuWave* g_wave;
-thread_local uint32_t g_lane;
-}  // namespace lz4e
+thread_local dim3 threadIdx;
 
-void emu_launch(uint32_t nblocks, std::function<void()> lane_body) {
+void emu_launch(uint32_t nblocks, uint32_t threads, std::function<void()> body) {
+    const uint32_t nw = (threads + 63) / 64;
     for (uint32_t b = 0; b < nblocks; ++b) {
         blockIdx = dim3(b);
-        lz4e::EmuWave w;
-        lz4e::g_wave = &w;
+        std::unique_ptr<EmuWave[]> waves(new EmuWave[nw]);
+        std::barrier<> group((std::ptrdiff_t)(64 * nw));
         memset(lz4e::smem, 0xA5, sizeof(lz4e::smem));  // LDS is not zeroed on the GPU
         std::vector<std::thread> th;
-        for (uint32_t l = 0; l < 64; ++l)
-            th.emplace_back([&, l]() {
-                lz4e::g_lane = l;
-                lane_body();
+        for (uint32_t t = 0; t < 64 * nw; ++t)
+            th.emplace_back([&, t]() {
+                g_emu_wave = &waves[t / 64];
+                g_emu_lane = t % 64;
+                g_emu_group = &group;
+                threadIdx = dim3(t);
+                body();
             });
-        for (auto& t : th) t.join();
+        for (auto& x : th) x.join();
     }
 }
 

@@ -1,6 +1,8 @@
 // Standalone driver of the lane emulator (sanitizer runs, debuggers):
 //   emu_main BLOCK_FILE TABLE_CLASS [FRAME_OUT [DICT_FILE]]
 //   emu_main -d FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (one-wave decoder)
+//   emu_main -p FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (pipelined decoder,
+//            4 waves: parser + 3 copiers)
 // compresses one block through the unmodified kernel source, prints the
 // return value and the iterator post-state words, and writes the frame.
 // With DICT_FILE the block is compressed in dictionary mode against the
@@ -31,9 +33,11 @@ static std::vector<uint8_t> slurp(const char* path) {
     return v;
 }
 
-extern "C" int emu_decompress_batch(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
-                                    uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
-                                    int32_t* ret, uint32_t nblocks, const int32_t* dict_len);
+extern "C" int emu_decode_results(const int32_t* ret, uint32_t n, char* err, uint32_t err_cap);
+extern "C" int emu_decompress_batch_mode(const uint8_t* src, const uint64_t* src_off,
+                                         const int32_t* src_len, uint8_t* dst, const uint64_t* dst_off,
+                                         const int32_t* dst_cap, int32_t* ret, uint32_t nblocks,
+                                         const int32_t* dict_len, uint32_t mode);
 
 // Decode: the frame in an exactly sized buffer, the output buffer exactly
 // [dictionary (last <= 64 KiB) | capacity] -- ASan sees any read before the
@@ -53,8 +57,11 @@ static int decode_main(int argc, char** argv) {
     // the decoder reads the input window by aligned dwords (the GPU's word
     // granularity: the dword holding the last byte); the heap block covers it
     frame.reserve((frame.size() + 3) & ~(size_t)3);
-    emu_decompress_batch(frame.data(), &so, &csize, out.data(), &doff, &cap, &ret, 1, &D);
-    printf("ret %d\n", ret);
+    const uint32_t mode = argv[1][1] == 'p' ? 2u : 1u;  // kDecPipe / kDecWave
+    emu_decompress_batch_mode(frame.data(), &so, &csize, out.data(), &doff, &cap, &ret, 1, &D, mode);
+    char err[256];
+    const int good = emu_decode_results(&ret, 1, err, sizeof err);
+    printf("ret %d\nresults %d %s\n", ret, good, err);
     if (argc > 4 && ret > 0) {
         FILE* o = fopen(argv[4], "wb");
         if (!o) return 2;
@@ -65,7 +72,8 @@ static int decode_main(int argc, char** argv) {
 }
 
 int main(int argc, char** argv) {
-    if (argc > 3 && argv[1][0] == '-' && argv[1][1] == 'd') return decode_main(argc, argv);
+    if (argc > 3 && argv[1][0] == '-' && (argv[1][1] == 'd' || argv[1][1] == 'p'))
+        return decode_main(argc, argv);
     if (argc < 3) {
         fprintf(stderr, "usage: emu_main BLOCK_FILE TABLE_CLASS [FRAME_OUT]\n");
         return 2;
