@@ -382,6 +382,58 @@ def single_call(threads_list=(1, 4, 16), calls: int = 400) -> dict:
     return res
 
 
+def block_floor(b: "Batch", top: int = 8, reps: int = 5) -> dict:
+    """The per-block floor of a step: the slowest blocks' compress + decode
+    time with the chip to themselves.  A stamped compress pass (per-block
+    cycle counters, lz4e_debug_compress_stamped) names the `top` slowest
+    blocks; each is then compressed and decoded alone (one-block launches,
+    HIP events on the batch's stream, best of `reps`).  However many GPUs
+    share the corpus, a step cannot be shorter than this: strong scaling's
+    ceiling is step(N=1) / floor."""
+    import ctypes
+
+    import torch
+
+    import lz4e_amd
+    L = lz4e_amd.lib()
+    P = ctypes.c_void_p
+    L.lz4e_debug_compress_stamped.argtypes = [P] * 8 + [ctypes.c_uint32, ctypes.c_uint32, P, P]
+    dbg = torch.zeros(b.nblk * 8, dtype=torch.int64, device=b.dev)
+    rc = L.lz4e_debug_compress_stamped(b.d_src.data_ptr(), b.d_off.data_ptr(), b.d_len.data_ptr(),
+                                       b.d_tt.data_ptr(), b.d_dst.data_ptr(), b.d_doff.data_ptr(),
+                                       b.d_cap.data_ptr(), b.d_ret.data_ptr(), b.nblk, b.bs,
+                                       b.stream.cuda_stream, dbg.data_ptr())
+    torch.cuda.synchronize(b.dev)
+    if rc != 0:
+        raise SystemExit("bench: stamped compress failed: " + lz4e_amd.last_error())
+    cyc = dbg.view(b.nblk, 8)[:, :6].sum(1).cpu().numpy()
+    worst = []
+    for i in np.argsort(cyc)[::-1][:top]:
+        i = int(i)
+        sl = slice(i, i + 1)
+        best_c, best_d = 1e9, 1e9
+        for _ in range(reps):
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record(b.stream)
+            lz4e_amd.compress_batch_dev(b.d_src, b.d_off[sl], b.d_len[sl], b.d_tt[sl], b.d_dst,
+                                        b.d_doff[sl], b.d_cap[sl], b.d_ret[sl], max_len=b.bs,
+                                        stream=b.stream.cuda_stream)
+            e1.record(b.stream)
+            lz4e_amd.decompress_batch_dev(b.d_dst, b.d_doff[sl], b.d_ret[sl], b.d_out, b.d_off[sl],
+                                          b.d_len[sl], b.d_dret[sl], stream=b.stream.cuda_stream,
+                                          max_cap=b.bs)
+            e2.record(b.stream)
+            torch.cuda.synchronize(b.dev)
+            best_c, best_d = min(best_c, e0.elapsed_time(e1)), min(best_d, e1.elapsed_time(e2))
+        worst.append((best_c + best_d, best_c, best_d, i, int(cyc[i])))
+    worst.sort(reverse=True)
+    t, tc, td, i, c = worst[0]
+    return {"floor_ms": round(t, 4), "compress_ms": round(tc, 4), "decompress_ms": round(td, 4),
+            "block": i, "stamped_cycles_in_full_launch": c,
+            "method": f"the {top} blocks with the most stamped compress cycles, each compressed and "
+                      f"decoded alone (best of {reps}); the slowest sum is the floor"}
+
+
 def strong_scaling(args, rank, world, dist, dev, bs, cls, gen, threads) -> dict:
     """The one corpus of the default block count, dealt over the ranks as a
     chunk queue, calibrated, rebalanced over RCCL, then timed."""
@@ -561,12 +613,19 @@ def main():
 
     # ---- strong scaling: one corpus over the N ranks (chunk queue) -------------
     if not args.no_strong:
+        # the step's per-block floor (after the timed region; rank 0's corpus
+        # is the N=1 corpus): the strong line cannot exceed step(N=1) / floor
+        floor = block_floor(b) if rank == 0 else None
         if world > 1:
             result["strong"] = strong_scaling(args, rank, world, dist, dev, bs, cls, gen, threads)
         else:
             result["strong"] = {"scaling": "strong", "blocks": nblk, "value": round(value, 3),
                                 "unit": "GiB/s", "ms_per_step": round(step_s * 1e3, 3),
                                 "note": "N=1: the same corpus as value"}
+        if floor is not None:
+            result["strong"]["block_floor"] = floor
+            # rank 0's weak-line step is one full corpus on one GPU: step(N=1)
+            result["strong"]["ceiling_x"] = round(step_s * 1e3 / floor["floor_ms"], 3)
 
     # ---- end to end through the chunk layer (PCIe-inclusive, never `value`) ----
     if world == 1 and not args.no_e2e:

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -419,6 +420,80 @@ int compress_sg_batch_impl(struct lz4e_sg_request* reqs, int n, const char* cons
     return ok;
 }
 
+// ---------------------------------------------------------------------------
+// Coalescing of concurrent single calls.  The reference is called once per
+// WRITE bio, synchronously, from every submitting CPU (lz4e_dev.c:174 ->
+// lz4e_req.c:177 -> lz4e_chunk.c:139-159), and a lone block is one wave's
+// serial parse on the GPU (~0.1-0.2 ms): calls that arrive while others are
+// in flight are worth one launch together.  Leader / follower batching: a
+// caller queues its request; when fewer than kMaxInflight batches are in
+// flight, it takes every queued request (its own included, up to kMaxBatch)
+// and runs them as one batch on its own thread -- the same batch entry point
+// as lz4e_compress_sg_batch / lz4e_decompress_batch, with identical bytes --
+// while the others wait for their result.  A lone caller always leads its
+// own one-request batch at once, so single-thread latency does not change.
+// ---------------------------------------------------------------------------
+template <class Req>
+struct Coalescer {
+    static constexpr int kMaxInflight = 4;    // concurrent batches (= HW queues of the process)
+    static constexpr size_t kMaxBatch = 1024;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<Req*> pending;
+    int inflight = 0;
+
+    template <class Run>
+    void submit(Req* r, Run run) {
+        std::unique_lock<std::mutex> lk(mu);
+        pending.push_back(r);
+        while (!r->done) {
+            if (!r->taken && inflight < kMaxInflight) {
+                std::vector<Req*> batch;
+                batch.push_back(r);
+                for (Req* q : pending)
+                    if (q != r && batch.size() < kMaxBatch) batch.push_back(q);
+                for (Req* q : batch) q->taken = true;
+                std::vector<Req*> rest;
+                for (Req* q : pending)
+                    if (!q->taken) rest.push_back(q);
+                pending.swap(rest);
+                inflight++;
+                lk.unlock();
+                run(batch);
+                lk.lock();
+                inflight--;
+                for (Req* q : batch) q->done = true;
+                cv.notify_all();
+            } else {
+                cv.wait(lk);
+            }
+        }
+    }
+};
+
+struct CompressCall {
+    lz4e_sg_request q;
+    bool taken = false, done = false;
+    std::string err;
+};
+
+struct DecompressCall {
+    const char* src;
+    char* dst;
+    int csize, cap, ret = -1;
+    bool taken = false, done = false;
+    std::string err;
+};
+
+Coalescer<CompressCall>& compress_calls() {
+    static Coalescer<CompressCall> c;
+    return c;
+}
+Coalescer<DecompressCall>& decompress_calls() {
+    static Coalescer<DecompressCall> c;
+    return c;
+}
+
 }  // namespace
 
 extern "C" {
@@ -431,9 +506,20 @@ int LZ4E_compress_default(const struct bio_vec* src, struct bio_vec* dst, struct
                           struct bvec_iter* dstIter, void* wrkmem) {
     if (wrkmem) std::memset(wrkmem, 0, LZ4E_MEM_COMPRESS);  // lz4e_compress.c:548
     if (srcIter->bi_size > LZ4E_MAX_INPUT_SIZE) return 0;
-    lz4e_sg_request q{src, dst, srcIter, dstIter, 0};
-    const int r = lz4e_compress_sg_batch(&q, 1);
-    return r < 0 ? 0 : q.ret;
+    CompressCall call;
+    call.q = lz4e_sg_request{src, dst, srcIter, dstIter, 0};
+    compress_calls().submit(&call, [](std::vector<CompressCall*>& batch) {
+        std::vector<lz4e_sg_request> reqs;
+        reqs.reserve(batch.size());
+        for (CompressCall* c : batch) reqs.push_back(c->q);
+        const int r = compress_sg_batch_impl(reqs.data(), (int)reqs.size(), nullptr, nullptr);
+        for (size_t i = 0; i < batch.size(); ++i) {
+            batch[i]->q.ret = r < 0 ? 0 : reqs[i].ret;
+            batch[i]->err = g_err;
+        }
+    });
+    g_err = call.err;
+    return call.q.ret;
 }
 
 int lz4e_compress_sg_batch_dict(struct lz4e_sg_request* reqs, int n, const char* const* dicts,
@@ -553,11 +639,29 @@ int lz4e_decompress_batch(const char* const* src, const int* csize, char* const*
 }
 
 int LZ4E_decompress_safe(const char* source, char* dest, int compressedSize, int maxDecompressedSize) {
-    int r = -1;
-    char* d = dest;
-    if (lz4e_decompress_batch(&source, &compressedSize, &d, &maxDecompressedSize, &r, 1) < 0)
-        return r < 0 ? r : -1;
-    return r;
+    DecompressCall call{source, dest, compressedSize, maxDecompressedSize};
+    decompress_calls().submit(&call, [](std::vector<DecompressCall*>& batch) {
+        const size_t n = batch.size();
+        std::vector<const char*> src(n);
+        std::vector<char*> dst(n);
+        std::vector<int> cs(n), cap(n), ret(n, -1);
+        for (size_t i = 0; i < n; ++i) {
+            src[i] = batch[i]->src;
+            dst[i] = batch[i]->dst;
+            cs[i] = batch[i]->csize;
+            cap[i] = batch[i]->cap;
+        }
+        const int r = decompress_batch_impl(src.data(), cs.data(), dst.data(), cap.data(), ret.data(),
+                                            (int)n, nullptr, nullptr);
+        for (size_t i = 0; i < n; ++i) {
+            // a failed call: the block's own value if it has one (the
+            // watchdog's LZ4E_DECODE_ABORTED), else -1
+            batch[i]->ret = r < 0 ? (ret[i] < 0 ? ret[i] : -1) : ret[i];
+            batch[i]->err = g_err;
+        }
+    });
+    g_err = call.err;
+    return call.ret;
 }
 
 int lz4e_decompress_batch_dict(const char* const* src, const int* csize, char* const* dst,

@@ -527,15 +527,18 @@ def test_chunk_write_batch_fault_then_smaller_call(gpu):
 
 
 def test_single_calls_concurrent(gpu, test_files):
-    """LZ4E_compress_default / LZ4E_decompress_safe from 8 threads at once
+    """LZ4E_compress_default / LZ4E_decompress_safe from 16 threads at once
     (the reference is reentrant given distinct wrkmem and is called from
-    every submitting CPU): every result equals the oracle's."""
+    every submitting CPU, lz4e_dev.c:174 -> lz4e_req.c:177): concurrent
+    calls are coalesced into shared batch launches, and every result --
+    frame, iterator post-state, decoded bytes, error code -- equals the
+    oracle's for its own request."""
     import threading
-    rng = np.random.default_rng(5)
     pool = _corpus("mixed", 1 << 20, 5).tobytes()
     errors = []
 
     def worker(t):
+        rng = np.random.default_rng(500 + t)
         try:
             for k in range(25):
                 n = int(rng.integers(0, 20000)) if k % 5 else 4096
@@ -552,13 +555,23 @@ def test_single_calls_concurrent(gpu, test_files):
                 if r != er or dst.read_prefix(r) != ef:
                     errors.append(("compress", t, k, r, er))
                     continue
+                src2 = make_sg(blk, segs, shuffle_seed=k)
+                dst2 = make_sg(b"", [4096] * (-(-cap // 4096) or 1), capacity=cap)
+                oracle_ref.compress_sg(src2, dst2)
+                if src.it.as_tuple() != src2.it.as_tuple() or dst.it.as_tuple() != dst2.it.as_tuple():
+                    errors.append(("iterators", t, k))
                 d = gpu.decompress_safe(ef, n)
                 if d != (n, blk):
                     errors.append(("decompress", t, k, d[0]))
+                if k % 7 == 3 and len(ef) > 2:  # a truncated frame: the reference's error code
+                    want = oracle_ref.decompress(ef[:len(ef) // 2], n)[0]
+                    got = gpu.decompress_safe(ef[:len(ef) // 2], n)[0]
+                    if got != want:
+                        errors.append(("code", t, k, got, want))
         except Exception as e:  # noqa: BLE001 -- reported below
             errors.append(("exception", t, repr(e)))
 
-    th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(16)]
     for x in th:
         x.start()
     for x in th:
@@ -635,6 +648,41 @@ def test_full_size_every_frame(gpu, name):
     lens = np.full(n, bs, np.int64)
     lens[-1] = total - (n - 1) * bs
     _full_size(gpu, host, lens, bs, cls)
+
+
+def test_full_size_sg512_layout_every_frame(gpu):
+    """configs[3] in its own SG layout at full size: the 3234 Silesia-proxy
+    blocks of 64 KiB, each a list of 128 bio_vecs of 512 B at random in-page
+    offsets (pages in shuffled order), through lz4e_compress_sg_batch (host
+    gather, one launch, scatter into 1000-byte destination segments).  Every
+    frame and both iterators' post-state equal oracle_compress_sg's, the
+    reference's per-access SG walk (lz4e_compress.c:184-211 class rules,
+    lz4e_defs.h:352-585 accessors)."""
+    bs, n, seg = 65536, 3234, 512
+    data = corpus.silesia_proxy(n * bs, 0x5157)
+    rng = np.random.default_rng(0x512)
+    cap = compress_bound(bs)
+    pairs, offs_all = [], []
+    for i in range(n):
+        offs = [int(x) for x in rng.integers(0, 4096, bs // seg)]
+        offs_all.append(offs)
+        src = make_sg(data[i * bs:(i + 1) * bs].tobytes(), [seg] * (bs // seg), offsets=offs,
+                      shuffle_seed=i)
+        dst = make_sg(b"", [1000] * (-(-cap // 1000)), capacity=cap)
+        pairs.append((src, dst))
+    assert all(gpu.table_type(s) == BYU32 for s, _ in pairs[:8])
+    rets = gpu.compress_sg_batch(pairs)
+    bad = []
+    for i, ((s, d), r) in enumerate(zip(pairs, rets)):
+        # the oracle walks the same source pages from the start iterator
+        s.it.bi_size, s_after = bs, s.it.as_tuple()
+        s.it.bi_idx, s.it.bi_bvec_done = 0, 0
+        d2 = make_sg(b"", [1000] * (-(-cap // 1000)), capacity=cap)
+        er = oracle_ref.compress_sg(s, d2)
+        if r != er or d.read_prefix(r) != d2.read_prefix(er) or s_after != s.it.as_tuple() or \
+                d.it.as_tuple() != d2.it.as_tuple():
+            bad.append(i)
+    assert not bad, f"{len(bad)} frames differ, first {bad[:5]}"
 
 
 @pytest.mark.parametrize("kind", ["mixed", "text", "runs", "ints", "random", "small_alpha", "fio"])

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Compress A/B session: parity of the compress tests, the default bench,
+# and the stamped per-phase breakdown (tools/stamps.py).
+tag=${1:-cab}
+o=gpurun_out/$tag; mkdir -p $o
+step() { local name=$1 to=$2; shift 2; echo "== $name" >&2
+  timeout -k 10 "$to" "$@" > "$o/$name.log" 2>&1; local rc=$?
+  echo "== $name rc=$rc" >&2; tail -n 4 "$o/$name.log" >&2
+  if [ $rc -ne 0 ]; then echo "stopping after $name (rc=$rc)" >&2; exit $rc; fi; }
+step pytest 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "compress or kat or edge or full_size or dict or sg"
+B=(--steps 10 --warmup 3 --no-cpu-baseline --no-parity --no-e2e --no-single-call --no-strong)
+step bench 300 python -u bench.py "${B[@]}"
+step bench_t256 300 python -u bench.py --workload text256k "${B[@]}"
+step bench_fio 300 python -u bench.py --workload fio4k "${B[@]}"
+step stamps 300 python -u tools/stamps.py
