@@ -342,6 +342,25 @@ def test_full_size_roundtrip(gpu, cls, bs, kind):
 
 
 @pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE], ids=["wave", "pipe"])
+def test_decompress_huge_runs(gpu, mode):
+    """Blocks whose sequences are hundreds of MiB long: a 256 MiB run of one
+    byte (a single match whose length extension is ~1 MiB of 0xFF) and a
+    96 MiB literal run followed by a 160 MiB run.  Both decoders copy them
+    in HBM; on the pipelined one the other waves wait on that copy for
+    ~0.1 s, which the watchdog must not mistake for a hang (its count resets
+    on every heartbeat of the copy).  Frames from the oracle
+    (lz4e_compress.c restated), values and bytes checked in full."""
+    run = b"\xab" * (256 << 20)
+    rnd = np.random.default_rng(8).integers(0, 256, 96 << 20, dtype=np.uint8).tobytes()
+    blocks = [run, rnd + run[:160 << 20]]
+    frames = [oracle_ref.compress(b, BYU32)[1] for b in blocks]
+    r, outs = _gpu_decompress(gpu, frames, [len(b) for b in blocks], mode=mode)
+    for i, b in enumerate(blocks):
+        assert r[i] == len(b), (i, r[i])
+        assert outs[i] == b, i
+
+
+@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE], ids=["wave", "pipe"])
 @pytest.mark.parametrize("cap_extra", [0, 100000])
 def test_decompress_periodic_matches(gpu, cap_extra, mode):
     """Self-overlapping matches of every period 1..40 and lengths around
