@@ -1063,23 +1063,10 @@ LZ4E_DEV void stage_block(uint32_t* dstw, const uint8_t* src, uint32_t n, uint32
     }
 }
 
-#include "lz4e_window2.h"
-
-template <bool kStamps, bool kW2, class IMG>
+template <bool kStamps, class IMG>
 LZ4E_DEV void dispatch_class(const IMG& img, uint32_t* smem, uint32_t n, int tt, gu8* out,
                              uint32_t cap, int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg,
                              uint32_t lane, uint32_t D = 0, bool pp = true) {
-    if constexpr (kW2) {
-        if (D == 0) {  // 128-position windows (lz4e_window2.h)
-            if (tt == kByU32)
-                compress_block_w2<kByU32, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, pp);
-            else if (tt == kByU16)
-                compress_block_w2<kByU16, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, pp);
-            else
-                compress_block_w2<kByU64, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, pp);
-            return;
-        }
-    }
     if (tt == kByU32)
         compress_block<kByU32, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, D, pp);
     else if (tt == kByU16)
@@ -1088,7 +1075,7 @@ LZ4E_DEV void dispatch_class(const IMG& img, uint32_t* smem, uint32_t n, int tt,
         compress_block<kByU64, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, 0, pp);
 }
 
-template <bool kLdsInput, bool kStamps, bool kW2 = false>
+template <bool kLdsInput, bool kStamps>
 __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict__ src,
                                                       const uint64_t* __restrict__ src_off,
                                                       const uint32_t* __restrict__ src_len,
@@ -1140,7 +1127,7 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
         stage_block(inw, in, n, lane);
         block_sync();
         const LdsImage img{inw, n == 0 ? 0 : (n - 1) >> 2};
-        dispatch_class<kStamps, kW2>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane);
+        dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane);
     } else {
         block_sync();
         const uint8_t* base = in - D;
@@ -1167,7 +1154,7 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
                 if (blockIdx.x < nh) __builtin_amdgcn_s_setprio(3);
             }
         }
-        dispatch_class<kStamps, kW2>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane, D, pp);
+        dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane, D, pp);
     }
 }
 
@@ -1294,20 +1281,13 @@ hipError_t launch_compress_impl(const CompressBatch& a, hipStream_t stream, uint
     if (a.nblocks == 0) return hipSuccess;
     // LZ4E_COMPRESS_LDS_MAX (bytes) overrides the LDS staging limit (experiments).
     static const uint32_t lds_max = env_u32("LZ4E_COMPRESS_LDS_MAX", kMaxLdsInput);
-    // LZ4E_COMPRESS_W2=1: the parse in 128-position windows (lz4e_window2.h).
-    static const bool w2 = env_u32("LZ4E_COMPRESS_W2", 0) != 0;
     const bool lds_input = a.max_len <= lds_max && a.dict_len == nullptr;
     const dim3 grid(a.nblocks), block(kWave);
     const uint32_t lds = compress_lds_bytes(a.max_len, lds_input);
     if (lds_input) {
-        if (w2)
-            hipLaunchKernelGGL((compress_kernel<true, kStamps, true>), grid, block, lds, stream, a.src,
-                               a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                               a.aux, a.nblocks, a.max_len, dbg, a.dict_len, nullptr);
-        else
-            hipLaunchKernelGGL((compress_kernel<true, kStamps>), grid, block, lds, stream, a.src,
-                               a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                               a.aux, a.nblocks, a.max_len, dbg, a.dict_len, nullptr);
+        hipLaunchKernelGGL((compress_kernel<true, kStamps>), grid, block, lds, stream, a.src,
+                           a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
+                           a.aux, a.nblocks, a.max_len, dbg, a.dict_len, nullptr);
         return hipGetLastError();
     }
     // heavy blocks first (see weight_kernel)
@@ -1326,15 +1306,10 @@ hipError_t launch_compress_impl(const CompressBatch& a, hipStream_t stream, uint
         (void)hipGetLastError();  // a failed pool allocation only costs the ordering
         scratch = nullptr;
     }
-    const uint32_t* order = scratch ? (const uint32_t*)(scratch + a.nblocks) : nullptr;
-    if (w2)
-        hipLaunchKernelGGL((compress_kernel<false, kStamps, true>), grid, block, lds, stream, a.src,
-                           a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.aux, a.nblocks, a.max_len, dbg, a.dict_len, order);
-    else
-        hipLaunchKernelGGL((compress_kernel<false, kStamps>), grid, block, lds, stream, a.src,
-                           a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.aux, a.nblocks, a.max_len, dbg, a.dict_len, order);
+    hipLaunchKernelGGL((compress_kernel<false, kStamps>), grid, block, lds, stream, a.src,
+                       a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
+                       a.aux, a.nblocks, a.max_len, dbg, a.dict_len,
+                       scratch ? (const uint32_t*)(scratch + a.nblocks) : nullptr);
     const hipError_t err = hipGetLastError();
     if (scratch) (void)hipFreeAsync(scratch, stream);
     return err;

@@ -1023,10 +1023,15 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
 // order, "all batches <= k" read off three flags): the in-order counters
 // poll one word instead of three and were 10 % faster on silesia64k.  Every
 // wait is bounded (watchdog).
-constexpr uint32_t kPipeWaves = 4;
+// LZ4E_PIPE_WAVES: workgroup size of the pipelined decoder (parser + copiers;
+// experiments only -- 3 and 5 waves measured slower than 4).
+#ifndef LZ4E_PIPE_WAVES
+#define LZ4E_PIPE_WAVES 4
+#endif
+constexpr uint32_t kPipeWaves = LZ4E_PIPE_WAVES;
 constexpr uint32_t kCopiers = kPipeWaves - 1;
 constexpr uint32_t kPipeRecs = 4;
-constexpr uint32_t kPipeSpans = 5;
+constexpr uint32_t kPipeSpans = kCopiers + 2;  // see copy_fast's slot safety
 constexpr int32_t kPipeOut = 1024;                   // output bytes per fast batch
 constexpr uint32_t kPipeSpan = kPipeOut + 16 + 48;   // its span (16-B aligned start)
 constexpr uint16_t kCross = 0x8000;  // jump entry: 0x8000 | (source - F)
@@ -1142,11 +1147,12 @@ LZ4E_DEV bool spin(PipeLds& S, F ready, W watch, PipeStamps& st, int k) {
     return ok;
 }
 
-// A fast batch j (see above).  Slot safety with 3 copiers in round robin:
-// span slot j % 5 last held batch j-5, read by batches j-4 and j-3 (cross
-// gathers) and by its own store pass; j-3 was this wave's previous batch,
-// j-4's gather happened before `resolved` reached j-3 (this wave waited for
-// that), and j-5 was stored before this wave's batch j-3 could be.
+// A fast batch j (see above).  Slot safety with K copiers in round robin
+// and K + 2 spans: span slot j % (K+2) last held batch j-K-2, read by
+// batches j-K-1 and j-K (cross gathers) and by its own store pass; j-K was
+// this wave's previous batch, j-K-1's gather happened before `resolved`
+// reached j-K (this wave waited for that), and j-K-2 was stored before this
+// wave's batch j-K could be.
 template <bool kStamps>
 LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const int32_t* hdr,
                         const uint8_t* in, int32_t srcSize, uint8_t* gout, uint32_t lane,
@@ -1503,7 +1509,7 @@ constexpr uint32_t kPipeMinCap = 16384;
 // sequence count, estimated by its compressed size; frames within 1/16 of
 // their capacity (stored / incompressible data: a few long literal runs) are
 // the lightest.
-constexpr uint32_t kOrderMin = 256 * 6;  // one round of pipelined workgroups
+constexpr uint32_t kOrderMin = 256 * (24 / kPipeWaves);  // one round of pipelined workgroups
 struct DecodeWeight {
     const int32_t* src_len;
     const int32_t* dst_cap;

@@ -94,27 +94,6 @@ def test_emulated_kernel_sanitized(emu_exe, tmp_path, kind, n, cls):
     assert (int(fs), int(lr)) == (efs, elr)
 
 
-W2_CASES = CASES + [("text", 65536, BYU16), ("ints", 65536, BYU32), ("text", 30000, BYU16)]
-
-
-@pytest.mark.parametrize("kind,n,cls", W2_CASES, ids=[f"{k}-{n}-{c}" for k, n, c in W2_CASES])
-def test_emulated_kernel_w2_sanitized(emu_exe, tmp_path, kind, n, cls):
-    """The parse in 128-position windows (LZ4E_COMPRESS_W2=1,
-    csrc/lz4e_window2.h): frames and iterator post-state equal the oracle's."""
-    data = _block(kind, n, 11 + n).tobytes()
-    blk, frame = tmp_path / "blk.bin", tmp_path / "frame.bin"
-    blk.write_bytes(data)
-    out = subprocess.run([emu_exe, str(blk), str(cls), str(frame)], capture_output=True, text=True,
-                         timeout=300, env=dict(os.environ, LZ4E_COMPRESS_W2="1"))
-    assert out.returncode == 0, out.stderr[-2000:]
-    assert "ERROR: AddressSanitizer" not in out.stderr and "runtime error" not in out.stderr
-    _, r, _, fs, lr = out.stdout.split()
-    er, ef, efs, elr = oracle_ref.compress(data, cls)
-    assert int(r) == er
-    assert frame.read_bytes() == ef
-    assert (int(fs), int(lr)) == (efs, elr)
-
-
 DICT_CASES = [("text", 4096, 4096), ("records", 16384, 65536), ("ints", 8192, 100000),
               ("text", 20000, 9), ("text", 20000, 5), ("random", 5000, 3000), ("text", 12, 4096)]
 
