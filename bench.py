@@ -15,7 +15,8 @@ Default workload (configs[1] of BASELINE.json): Silesia-proxy, 3234 blocks of
 64 KiB (~212 MB, the Silesia size) per GPU, each block a 16 x 4 KiB bio_vec
 list (byU16 hash table).  Other workloads (--workload) are the parity
 configurations: fio4k (configs[2]), sg512 (configs[3], byU32), text256k
-(configs[4]).
+(configs[4]; its line adds ``decompress_only``, the frames decoded alone as
+that configuration asks, weak and strong over the ranks).
 
 Multi-GPU: ``python bench.py --gpus N`` starts N ranks itself (through
 torch.distributed.run, before anything touches a GPU); under an external
@@ -75,6 +76,8 @@ def parse():
     ap.add_argument("--no-single-call", action="store_true", help="skip the single-call latency leg")
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling line")
     ap.add_argument("--no-parity", action="store_true", help="skip the every-frame oracle check")
+    ap.add_argument("--no-decompress-only", action="store_true",
+                    help="text256k: skip the decompress-only leg (configs[4])")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check only: start the ranks (gloo), report, touch no GPU")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -434,6 +437,72 @@ def block_floor(b: "Batch", top: int = 8, reps: int = 5) -> dict:
                       f"decoded alone (best of {reps}); the slowest sum is the floor"}
 
 
+def decompress_only(b: "Batch", steps: int, rank: int, world: int, dist, dev, traffic_json: str,
+                    workload: str) -> dict:
+    """configs[4] ("Decompress-only, enwik9 at 256 KiB blocks, 8 x MI355X"):
+    the frames of the last compress, already in HBM, decoded alone -- `steps`
+    timed launches between a barrier + synchronize on both sides, the max
+    over ranks.  Two lines:
+    * weak: every rank decodes all of its corpus (N corpora);
+    * strong: the one job of b.nblk blocks dealt over the ranks as contiguous
+      slices of the block list (rank r decodes blocks [r n/N, (r+1) n/N) of
+      its corpus; same generator, so the slices are alike) -- blocks are
+      independent, so there is no data-path collective.
+    Roofline: algorithmic C + U bytes of one launch / its mean duration."""
+    import torch
+    import lz4e_amd
+    from lz4e_amd.shards import reduce_step
+    group = dist.group.WORLD if dist else None
+    sizes = b.rets.astype(np.int64)
+
+    def timed(sl) -> float:
+        args_ = (b.d_dst, b.d_doff[sl], b.d_ret[sl], b.d_out, b.d_off[sl], b.d_len[sl], b.d_dret[sl])
+        for _ in range(2):  # warm-up launches
+            lz4e_amd.decompress_batch_dev(*args_, stream=b.stream.cuda_stream, max_cap=b.max_cap)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(b.stream)
+        for _ in range(steps):
+            lz4e_amd.decompress_batch_dev(*args_, stream=b.stream.cuda_stream, max_cap=b.max_cap)
+        e1.record(b.stream)
+        torch.cuda.synchronize(dev)
+        if dist:
+            dist.barrier()
+        return e0.elapsed_time(e1) / steps
+
+    traffic = None
+    if os.path.exists(traffic_json):
+        try:
+            traffic = json.load(open(traffic_json)).get(workload, {}).get("decompress")
+        except (OSError, ValueError):
+            traffic = None
+    out = {"kernel": "decompress", "steps": steps}
+    # weak: all blocks on every rank
+    ms = timed(slice(0, b.nblk))
+    if not (b.d_dret.cpu().numpy() == b.lens).all():
+        raise SystemExit("bench: decompress-only leg decoded wrong sizes")
+    (ms_max,), C_all = reduce_step([ms], int(sizes.sum()), group, dev)
+    U, C = int(b.lens.sum()), int(sizes.sum())
+    out["weak"] = {"value": round(U * world / (ms_max / 1e3) / 2**30, 3), "unit": "GiB/s",
+                   "ms_per_step": round(ms_max, 4), "blocks_per_gpu": b.nblk,
+                   "roofline": {"bound": "hbm", "achieved": round((U + C) / (ms / 1e3) / 1e9, 2),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": round((U + C) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
+                                "traffic": traffic, "algorithmic_bytes_per_launch": U + C}}
+    # strong: one job of b.nblk blocks over the ranks
+    lo, hi = rank * b.nblk // world, (rank + 1) * b.nblk // world
+    ms_s = timed(slice(lo, hi)) if hi > lo else 0.0
+    (ms_s_max,), _ = reduce_step([ms_s], 0, group, dev)
+    out["strong"] = {"value": round(U / (ms_s_max / 1e3) / 2**30, 3) if ms_s_max > 0 else None,
+                     "unit": "GiB/s", "ms_per_step": round(ms_s_max, 4), "blocks_job": b.nblk,
+                     "blocks_this_rank": hi - lo,
+                     "note": "rank r decodes blocks [r n/N, (r+1) n/N) of its corpus (same generator)"}
+    return out
+
+
 def strong_scaling(args, rank, world, dist, dev, bs, cls, gen, threads) -> dict:
     """The one corpus of the default block count, dealt over the ranks as a
     chunk queue, calibrated, rebalanced over RCCL, then timed."""
@@ -610,6 +679,11 @@ def main():
         "decompress_GiBps": round(U_all / (dec_ms / 1e3) / 2**30, 3),
         "roofline": roofline,
     }
+
+    # ---- configs[4]: decompress-only (the HBM-roofline stress run) -------------
+    if args.workload == "text256k" and not args.no_decompress_only:
+        result["decompress_only"] = decompress_only(b, args.steps, rank, world, dist, dev,
+                                                    args.traffic_json, args.workload)
 
     # ---- strong scaling: one corpus over the N ranks (chunk queue) -------------
     if not args.no_strong:
