@@ -606,12 +606,21 @@ LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_
     // positions 4l..4l+3) are composed with ds_bpermute gathers, then lane k
     // follows the bits of k to token k.  Every field and check is then
     // evaluated per lane.
-    if (ip <= iend - 18 && op <= oend - 32) {
+    bool fast = ip <= iend - 18 && op <= oend - 32;
+    uint32_t wv = 0;
+    if (fast) {
         win.follow(ip);
+        wv = win.rd4(ip + 4 * (int32_t)lane);
+        // A batch that starts at a token with extension bytes -- every such
+        // token ends the fast batch before it -- is the scalar path's: lane
+        // 0's token would fail `cand` below, so no tables are composed.
+        const uint32_t t0 = lane_val(wv, 0) & 0xFFu;
+        fast = (t0 >> 4) != 15 && (t0 & 15) != 15;
+    }
+    if (fast) {
         const int32_t r0 = ip - win.base;                  // < 256
         const int32_t rin = iend - 18 - win.base;          // last token offset on the fast path
         const int32_t jlim = (rin < 494 ? rin : 494) - r0;  // (offset bytes stay in A+B)
-        const uint32_t wv = win.rd4(ip + 4 * (int32_t)lane);
         uint32_t J[6];
         {
             uint32_t j1 = 0;
