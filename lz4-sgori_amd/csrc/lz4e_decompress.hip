@@ -1190,9 +1190,11 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
     }
     const bool lfast = valid && b.L > 0 && b.ls + 16 <= srcSize;
     if (lfast) lv = ldg16(in + b.ls);
-    // every byte of [lo, hi) final until shown otherwise
-#pragma unroll 4
-    for (int32_t i = s0 + (int32_t)lane; i < s1; i += kWave) jt[i] = kFinal;
+    // every byte of [lo, hi) final until shown otherwise: 4 entries per
+    // 8-byte store (the row is 16-byte aligned; entries outside [lo, hi) are
+    // never read as pointers -- `entry` masks them)
+    for (int32_t g = (s0 & ~3) + 4 * (int32_t)lane; g < s1; g += 4 * (int32_t)kWave)
+        *(lu64*)(jt + g) = ~0ull;
     wave_fence();
     // match bytes [nf, M): a cross pointer below lo, else an internal one
     const bool ptrs = valid && b.off != 0 && nf < b.M;
