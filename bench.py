@@ -456,9 +456,15 @@ def decompress_only(b: "Batch", steps: int, rank: int, world: int, dist, dev, tr
     sizes = b.rets.astype(np.int64)
 
     def timed(sl) -> float:
+        # every rank passes both barriers, an empty slice included
         args_ = (b.d_dst, b.d_doff[sl], b.d_ret[sl], b.d_out, b.d_off[sl], b.d_len[sl], b.d_dret[sl])
+        n = sl.stop - sl.start
+
+        def launch():
+            if n > 0:
+                lz4e_amd.decompress_batch_dev(*args_, stream=b.stream.cuda_stream, max_cap=b.max_cap)
         for _ in range(2):  # warm-up launches
-            lz4e_amd.decompress_batch_dev(*args_, stream=b.stream.cuda_stream, max_cap=b.max_cap)
+            launch()
         torch.cuda.synchronize(dev)
         if dist:
             dist.barrier()
@@ -466,12 +472,12 @@ def decompress_only(b: "Batch", steps: int, rank: int, world: int, dist, dev, tr
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(b.stream)
         for _ in range(steps):
-            lz4e_amd.decompress_batch_dev(*args_, stream=b.stream.cuda_stream, max_cap=b.max_cap)
+            launch()
         e1.record(b.stream)
         torch.cuda.synchronize(dev)
         if dist:
             dist.barrier()
-        return e0.elapsed_time(e1) / steps
+        return e0.elapsed_time(e1) / steps if n > 0 else 0.0
 
     traffic = None
     if os.path.exists(traffic_json):
@@ -494,7 +500,7 @@ def decompress_only(b: "Batch", steps: int, rank: int, world: int, dist, dev, tr
                                 "traffic": traffic, "algorithmic_bytes_per_launch": U + C}}
     # strong: one job of b.nblk blocks over the ranks
     lo, hi = rank * b.nblk // world, (rank + 1) * b.nblk // world
-    ms_s = timed(slice(lo, hi)) if hi > lo else 0.0
+    ms_s = timed(slice(lo, hi))
     (ms_s_max,), _ = reduce_step([ms_s], 0, group, dev)
     out["strong"] = {"value": round(U / (ms_s_max / 1e3) / 2**30, 3) if ms_s_max > 0 else None,
                      "unit": "GiB/s", "ms_per_step": round(ms_s_max, 4), "blocks_job": b.nblk,

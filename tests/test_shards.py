@@ -7,6 +7,7 @@ oracle (the checker stands in for the per-rank codec: no GPU on this host) and
 the job's concatenated frame stream must equal the single-process one."""
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -305,3 +306,67 @@ def test_two_rank_gloo_strong_scaling_calls(tmp_path):
     for b in range(n):
         src = text if b // chunk in owner0 else rnd
         assert frames[b] == oracle_ref.compress(src[b * bs:(b + 1) * bs].tobytes(), BYU16)[1]
+
+
+def _donly_worker(rank, world, port, nblk, out_dir):
+    """bench.decompress_only on `world` gloo ranks with the GPU calls faked
+    (the decode fills its size slots; events report 1 ms): every rank passes
+    the same barriers -- a rank whose strong slice is empty included -- and
+    all ranks report the same max-over-ranks lines."""
+    import json
+    import types
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import lz4e_amd
+
+    class Ev:
+        def __init__(self, enable_timing=True):
+            pass
+
+        def record(self, stream=None):
+            pass
+
+        def elapsed_time(self, other):
+            return 1.0 * (1 + rank)  # rank r is (r + 1)x slower
+
+    torch.cuda.Event = Ev
+    torch.cuda.synchronize = lambda *a, **k: None
+    calls = []
+
+    def fake_decode(src, src_off, src_len, dst, dst_off, dst_cap, ret, stream=None, max_cap=None):
+        calls.append(int(src_len.numel()))
+        ret.copy_(dst_cap)
+
+    lz4e_amd.decompress_batch_dev = fake_decode
+    lens = np.full(nblk, 1000, dtype=np.int64)
+    t = lambda a, dt: torch.from_numpy(np.asarray(a).astype(dt))
+    b = types.SimpleNamespace(
+        nblk=nblk, lens=lens, rets=np.full(nblk, 400, dtype=np.int32), max_cap=1000,
+        d_dst=torch.zeros(1), d_out=torch.zeros(1), stream=types.SimpleNamespace(cuda_stream=0),
+        d_doff=t(np.zeros(nblk), np.int64), d_ret=t(np.full(nblk, 400), np.int32),
+        d_off=t(np.zeros(nblk), np.int64), d_len=t(lens, np.int32), d_dret=t(np.zeros(nblk), np.int32))
+    out = bench.decompress_only(b, 3, rank, world, dist, torch.device("cpu"), "", "text256k")
+    out["calls"] = calls
+    with open(os.path.join(out_dir, f"d{rank}.json"), "w") as f:
+        json.dump(out, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_decompress_only_leg(tmp_path):
+    """configs[4]'s decompress-only leg over two ranks, one block: rank 0's
+    strong slice is empty (no launch) and rank 1 decodes the block; both
+    reach the end, the weak and strong lines are the max over ranks."""
+    import json
+    world = 2
+    mp.spawn(_donly_worker, args=(world, _free_port(), 1, str(tmp_path)), nprocs=world, join=True)
+    r = [json.load(open(tmp_path / f"d{k}.json")) for k in range(world)]
+    assert r[0]["weak"] == r[1]["weak"] and r[0]["strong"]["value"] == r[1]["strong"]["value"]
+    assert r[0]["weak"]["ms_per_step"] == round(2.0 / 3, 4)  # max over ranks: 2 ms / 3 steps
+    assert [x["strong"]["blocks_this_rank"] for x in r] == [0, 1]
+    # weak: 2 warm-up + 3 timed launches of the whole batch on each rank;
+    # strong: none on the empty rank, 5 of one block on the other
+    assert r[0]["calls"] == [1] * 5 and r[1]["calls"] == [1] * 10
