@@ -1130,8 +1130,8 @@ struct PipeStamps {
 // Waits until ready(); false when the watchdog fired (here or in another
 // wave).  watch() is the LDS counter the wait depends on: the watchdog
 // counts sleeps since it last moved.
-template <class F, class W>
-LZ4E_DEV bool wait_for(PipeLds& S, F ready, W watch) {
+template <class SL, class F, class W>
+LZ4E_DEV bool wait_for(SL& S, F ready, W watch) {
     int32_t last = watch();
     for (uint32_t k = 0; !ready(); ++k) {
         const int32_t now = watch();
@@ -1511,6 +1511,404 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
     }
 }
 
+// ============================================================================
+// Streaming decoder: one block per 2-wave workgroup
+// ============================================================================
+//
+// Wave 0 parses exactly as in the pipelined decoder and publishes each batch
+// (records, output range, and for a fast batch the 512 input bytes of its
+// parse window) in a ring of record slots.  Wave 1 writes the output in
+// order, 256 bytes per step, lane l owning the dword at step offset 4l:
+//
+//  * owners: each sequence starting in the step marks its dword (LDS), a DPP
+//    max-scan gives every dword the last sequence started at or before it;
+//    a dword holds at most one sequence start (every fast sequence has a
+//    match of 4+ bytes), so two owners and four ds_bpermute gathers of the
+//    packed fields serve its four bytes;
+//  * sources: a literal byte comes from the slot's input window, a match
+//    byte from out[x - off] -- in LDS (an R-byte history ring of the output),
+//    in HBM when further back (stored earlier by this same wave, so in order:
+//    one vector L1 per CU), or in the step itself (pointer jumping over the
+//    step's 256 bytes, a chain of depth d in log2 d rounds); offset 0 writes
+//    zeros (lz4e_decompress.c:313, 407-415);
+//  * one dword per lane into the ring and one into HBM (byte stores only at
+//    the batch's two ends, so exactly [lo, hi) is written).
+//
+// No cross-wave ordering beyond the record slots: one wave writes every
+// output byte in order, so a source is final once its step has run.  A
+// scalar-path batch (long runs, block ends) copies in HBM as before, then
+// reloads the ring's last R bytes from HBM.  LDS ~11 KiB per block.
+#ifndef LZ4E_STREAM_RING
+#define LZ4E_STREAM_RING 4096
+#endif
+#ifndef LZ4E_STREAM_RECS
+#define LZ4E_STREAM_RECS 3
+#endif
+constexpr int32_t kSRing = LZ4E_STREAM_RING;  // power of two, >= 512
+constexpr uint32_t kSRecs = LZ4E_STREAM_RECS;
+constexpr int32_t kSOut = 2047;  // output bytes per fast batch (11-bit packed fields)
+constexpr int32_t kSStep = 4 * kWave;
+static_assert((kSRing & (kSRing - 1)) == 0 && kSRing >= 2 * kSStep, "ring size");
+enum { kSN, kSKind, kSLo, kSHi, kSBase, kSWords = 8 };
+
+struct StreamLds {
+    uint32_t ring[(kRing + kRingPad) / 4];  // parser input ring
+    int32_t rec[kSRecs][5][kWave];          // ls, L, op, off, M per sequence
+    int32_t hdr[kSRecs][kSWords];
+    uint32_t inp[kSRecs][2 * kWave];        // a fast batch's input window A|B (512 B)
+    uint32_t hist[kSRing / 4];              // output history ring
+    uint32_t mark[kWave];                   // per-step owner marks
+    uint64_t vp[kWave];                     // per-step (pointer << 8 | byte) x 4, pointer jumping
+    int32_t pub[kSRecs], con[kSRecs];
+    int32_t nb_total, abort, beat, result;
+};
+
+// Inclusive prefix max over the 64 lanes (values >= 0) with DPP.
+LZ4E_DEV uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+LZ4E_DEV uint32_t wave_incl_umax(uint32_t v) {
+    uint32_t x = v;
+    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
+    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
+    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
+    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
+    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
+    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
+    return x;
+}
+
+// Cycle counters of the stamped build (u64 per block): parser parse, parser
+// waits for a slot, copier waits for records, copier fast batches, copier
+// scalar batches (+ ring refill), batches, steps, steps with a far (HBM)
+// source, pointer-jumping rounds, steps with in-step sources.
+enum { kSsParse, kSsPWait, kSsRec, kSsFast, kSsScalar, kSsBatches, kSsSteps, kSsFarSteps,
+       kSsRounds, kSsPendSteps, kSsSlots };
+struct StreamStamps {
+    uint64_t t = 0, a[kSsSlots] = {};
+    LZ4E_DEV void lap(bool on, int k) {
+        if (!on) return;
+        const uint64_t now = clock64();
+        a[k] += now - t;
+        t = now;
+    }
+    LZ4E_DEV void add(bool on, int k, uint64_t v) {
+        if (on) a[k] += v;
+    }
+};
+
+// The HBM store of a step's dword, deferred by one step: issued after the
+// next step's far loads, so that those do not wait for it (a wave's loads and
+// stores complete in order).  bm: the bytes of the dword at x0 that belong to
+// the output (all four but at a batch's two ends).
+struct PendStore {
+    uint32_t v = 0, bm = 0;
+    int32_t x0 = 0;
+    LZ4E_DEV void flush(uint8_t* gout) {
+        if (bm == 0xFu) {
+            *(gu32w*)(gout + x0) = v;
+        } else if (bm) {
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q)
+                if ((bm >> q) & 1) *(gu8*)(gout + x0 + (int32_t)q) = (uint8_t)(v >> (8 * q));
+        }
+        bm = 0;
+    }
+};
+
+// A step's byte sources (see stream_fast): LDS byte addresses, pointers
+// into the step (0xFF: none), zero / far / own-byte masks, far positions and
+// the far bytes (loaded when the descriptor is built, one step ahead of use).
+struct StepDesc {
+    uint32_t ao[4], fl[4], PT, zm, fm, bm;
+};
+
+// The output of fast batch [lo, hi) (records in b, input window at ibase in
+// the slot), 256 bytes per step (see above).  Software-pipelined: step t+1's
+// descriptor (owners, fields, sources, far loads) is built while step t's
+// gathers are in flight.
+template <bool kStamps>
+LZ4E_DEV void stream_fast(StreamLds& S, uint32_t slot, const Batch& b, int32_t lo, int32_t hi,
+                          int32_t ibase, uint8_t* gout, uint32_t lane, PendStore& ps, StreamStamps& st) {
+    const bool valid = lane < b.n;
+    // packed fields of sequence k (lane k): output start, match start and
+    // literal source relative to the batch / its window; the offset
+    const uint32_t P1 = valid ? (uint32_t)(b.op - lo) | ((uint32_t)(b.op + b.L - lo) << 11) |
+                                    ((uint32_t)(b.ls - ibase) << 22)
+                              : 0u;
+    const uint32_t P2 = valid ? (uint32_t)b.off : 0u;
+    lu8* const sb = (lu8*)&S;
+    const uint32_t h0 = (uint32_t)((lu8*)S.hist - sb);
+    const uint32_t i0 = (uint32_t)((lu8*)S.inp[slot] - sb);
+    lu32* mark = (lu32*)S.mark;
+    int32_t carry = -1;  // owner of the byte before the step
+    auto describe = [&](int32_t Xs, StepDesc& d) {
+        const int32_t x0 = Xs + 4 * (int32_t)lane;
+        mark[lane] = 0;
+        lockstep();
+        const int32_t rs = b.op - Xs;
+        if (valid && rs >= 0 && rs < kSStep) mark[rs >> 2] = ((lane + 1) << 2) | (uint32_t)(rs & 3);
+        lockstep();
+        const uint32_t m = mark[lane];
+        const uint32_t Mx = wave_incl_umax(m);
+        const int32_t o2 = Mx ? (int32_t)(Mx >> 2) - 1 : carry;
+        carry = (int32_t)lane_val((uint32_t)o2, kWave - 1);
+        const int32_t o1 = m ? o2 - 1 : o2;
+        const uint32_t j = m ? (m & 3) : 0;  // bytes q >= j are o2's
+        const uint32_t c1 = (uint32_t)(o1 < 0 ? 0 : o1), c2 = (uint32_t)(o2 < 0 ? 0 : o2);
+        const uint32_t A1 = shfl(P1, c1), B1 = shfl(P2, c1), A2 = shfl(P1, c2), B2 = shfl(P2, c2);
+        const int32_t flo = Xs - kSRing + 4;  // sources below this (or < 0) are read from HBM
+        // every byte's source, branch-free: an LDS byte address (ring or
+        // input window), an HBM position (far), a step byte (pending) or zero
+        d.PT = 0;
+        d.zm = 0;
+        d.fm = 0;
+        d.bm = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const int32_t x = x0 + (int32_t)q;
+            const bool sec = q >= j;
+            const uint32_t A = sec ? A2 : A1, off = sec ? B2 : B1;
+            const int32_t xr = x - lo;
+            const int32_t op_r = (int32_t)(A & 0x7FFu), ms_r = (int32_t)((A >> 11) & 0x7FFu);
+            const int32_t ls_r = (int32_t)(A >> 22);
+            const bool before = xr < 0, past = x >= hi;
+            const bool lit = !before && xr < ms_r;
+            const bool mt = !before && !past && !lit;
+            const int32_t src = x - (int32_t)off;
+            const bool cp = mt && off != 0;
+            const bool pend = cp && src >= Xs;
+            const bool ring = cp && src < Xs && src >= flo && src >= 0;
+            const bool far = cp && !pend && !ring;
+            const uint32_t hx = h0 + (uint32_t)(x & (kSRing - 1)), hs = h0 + (uint32_t)(src & (kSRing - 1));
+            const uint32_t il = i0 + (uint32_t)(ls_r + xr - op_r);
+            d.ao[q] = before ? hx : (lit ? il : (ring ? hs : h0));
+            d.PT |= (pend ? (uint32_t)(src - Xs) : 0xFFu) << (8 * q);
+            d.zm |= (past || (mt && off == 0) ? 1u : 0u) << q;
+            d.fm |= (far ? 1u : 0u) << q;
+            d.bm |= (!before && !past ? 1u : 0u) << q;
+            // far byte (always loaded: a fixed number of loads per step keeps
+            // the compiler's waits exact; a non-far lane reads byte lo)
+            d.fl[q] = *(const gu8*)(gout + (far ? src : lo));
+        }
+    };
+    StepDesc cur, nxt;
+    int32_t Xs = lo & ~3;
+    describe(Xs, cur);
+    for (; Xs < hi; Xs += kSStep) {
+        const int32_t x0 = Xs + 4 * (int32_t)lane;
+        const bool more_steps = Xs + kSStep < hi;
+        if (more_steps) describe(Xs + kSStep, nxt);
+        ps.flush(gout);  // the previous step's dword (after the far loads)
+        lockstep();      // the previous step's ring dwords, read by other lanes
+        uint32_t g[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) g[q] = sb[cur.ao[q]];
+        if (kStamps) {
+            st.add(true, kSsSteps, 1);
+            st.add(true, kSsFarSteps, ballot(cur.fm != 0) != 0);
+            st.add(true, kSsPendSteps, ballot(cur.PT != 0xFFFFFFFFu) != 0);
+        }
+        uint32_t V = 0, PT = cur.PT;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t v = ((cur.fm >> q) & 1) ? cur.fl[q] : (((cur.zm >> q) & 1) ? 0u : g[q]);
+            V |= (v & 0xFFu) << (8 * q);
+        }
+        // in-step sources: pointer jumping (the pointer of byte t names the
+        // step byte it copies; 0xFF = final)
+        if (ballot(PT != 0xFFFFFFFFu)) {
+            const lu16* vt = (const lu16*)S.vp;
+            for (;;) {
+                uint64_t w = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q)
+                    w |= (uint64_t)((((PT >> (8 * q)) & 0xFFu) << 8) | ((V >> (8 * q)) & 0xFFu)) << (16 * q);
+                *(lu64*)&S.vp[lane] = w;
+                lockstep();
+                uint32_t e[4];
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t p = (PT >> (8 * q)) & 0xFFu;
+                    e[q] = vt[p == 0xFFu ? 0u : p];  // (unconditional: all in flight together)
+                }
+                uint32_t PN = 0, VN = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t p = (PT >> (8 * q)) & 0xFFu;
+                    const uint32_t tp = e[q] >> 8;
+                    PN |= (p == 0xFFu ? 0xFFu : tp) << (8 * q);
+                    VN |= ((p != 0xFFu && tp == 0xFFu) ? (e[q] & 0xFFu) : ((V >> (8 * q)) & 0xFFu)) << (8 * q);
+                }
+                PT = PN;
+                V = VN;
+                st.add(kStamps, kSsRounds, 1);
+                if (!ballot(PT != 0xFFFFFFFFu)) break;
+            }
+        }
+        lockstep();  // (every gather of the step before the ring write)
+        if (x0 < hi) *(lu32*)(sb + h0 + (uint32_t)(x0 & (kSRing - 1))) = V;
+        ps.v = V;
+        ps.x0 = x0;
+        ps.bm = cur.bm;
+        if (more_steps) cur = nxt;
+    }
+}
+
+// After an in-HBM batch [lo, hi): the history ring's bytes from HBM (the
+// copies were this wave's own stores: in order).
+LZ4E_DEV void stream_refill(StreamLds& S, int32_t lo, int32_t hi, const uint8_t* gout, uint32_t lane) {
+    int32_t g0 = (hi & ~3) - kSRing + 4;
+    g0 = (g0 > lo ? g0 : lo) & ~3;
+    lu8* hist = (lu8*)S.hist;
+    for (int32_t g = g0 + 4 * (int32_t)lane; g < hi; g += kSStep) {
+        uint32_t v = 0;
+        if (g + 4 <= hi) {
+            v = *(const gcu32*)(const void*)(gout + g);
+        } else {
+            for (int32_t q = 0; g + q < hi; ++q) v |= (uint32_t)gout[g + q] << (8 * q);
+        }
+        *(lu32*)(hist + (g & (kSRing - 1))) = v;
+    }
+    wave_fence();
+}
+
+// Streaming decoder kernel: LDS ~11 KiB and two waves per block, so a
+// whole 64 KiB-block batch of the Silesia size is resident at once.
+// (waves per SIMD: 7 = 14 two-wave blocks per CU, the LDS limit at ~11 KiB)
+#ifndef LZ4E_STREAM_WAVES_PER_EU
+#define LZ4E_STREAM_WAVES_PER_EU 7
+#endif
+template <bool kStamps>
+__global__ __launch_bounds__(2 * kWave, LZ4E_STREAM_WAVES_PER_EU) void decompress_stream_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
+    const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
+    uint64_t* __restrict__ dbg, const int32_t* __restrict__ dict_len,
+    const uint32_t* __restrict__ order) {
+    __shared__ __attribute__((aligned(16))) StreamLds S;
+    if (blockIdx.x >= nblocks) return;
+    const uint32_t b = order ? order[blockIdx.x] : blockIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+    const int32_t srcSize = src_len[b];
+    const int32_t outSize = dst_cap[b];
+    const uint8_t* in = src + src_off[b];
+    uint8_t* gout = dst + dst_off[b];
+    if (special_case(in, srcSize, outSize, ret + b, tid)) return;
+    StreamStamps st;
+    if (kStamps) st.t = clock64();
+    if (tid < kSRecs) {
+        S.pub[tid] = -1;
+        S.con[tid] = (int32_t)tid - (int32_t)kSRecs;
+    }
+    if (tid == 0) {
+        S.nb_total = INT32_MAX;
+        S.abort = 0;
+        S.beat = 0;
+        S.result = kPipeAbort;
+    }
+    __syncthreads();
+
+    if (wave == 0) {
+        // ---------------- parser (as in decompress_pipe_kernel) ----------------
+        __builtin_amdgcn_s_setprio(3);
+        Parse P;
+        P.init(in, srcSize, outSize, (lu32*)S.ring, lane, dict_of(dict_len, b));
+        int32_t j = 0;
+        for (;;) {
+            Batch bt;
+            const int32_t lo = P.op;
+            const ParseResult pr = parse_batch<true>(P, bt, lane, kSOut);
+            st.lap(kStamps, kSsParse);
+            if (pr == kParseFail) {
+                if (lane == 0) S.result = -P.ip - 1;
+                break;
+            }
+            const uint32_t slot = (uint32_t)j % kSRecs;
+            if (!wait_for(S, [&] { return lds_acquire(&S.con[slot]) == j - (int32_t)kSRecs; },
+                          [&] { return lds_acquire(&S.beat) + lds_acquire(&S.con[slot]); })) {
+                lds_release(&S.abort, 1);
+                break;
+            }
+            st.lap(kStamps, kSsPWait);
+            S.rec[slot][0][lane] = bt.ls;
+            S.rec[slot][1][lane] = bt.L;
+            S.rec[slot][2][lane] = bt.op;
+            S.rec[slot][3][lane] = bt.off;
+            S.rec[slot][4][lane] = bt.M;
+            if (pr == kParsedFast) {
+                S.inp[slot][lane] = P.win.a;
+                S.inp[slot][kWave + lane] = P.win.b;
+            }
+            if (lane < kSWords) {
+                const int32_t h[kSWords] = {(int32_t)bt.n, pr == kParsedScalar ? kKindHbm : kKindFast,
+                                            lo, P.op, P.win.base, 0, 0, 0};
+                int32_t v = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < kSWords; ++q) v = lane == q ? h[q] : v;
+                S.hdr[slot][lane] = v;
+            }
+            lds_release(&S.pub[slot], j);
+            j++;
+            if (P.done) {
+                if (lane == 0) S.result = P.op;
+                break;
+            }
+        }
+        lds_release(&S.nb_total, j);
+    } else {
+        // ---------------- copier ----------------
+        PendStore ps;
+        for (int32_t j = 0;; ++j) {
+            const uint32_t slot = (uint32_t)j % kSRecs;
+            const bool ok = wait_for(
+                S, [&] { return lds_acquire(&S.pub[slot]) == j || lds_acquire(&S.nb_total) <= j; },
+                [&] { return lds_acquire(&S.beat) + lds_acquire(&S.pub[slot]); });
+            st.lap(kStamps, kSsRec);
+            if (!ok) {
+                lds_release(&S.abort, 1);
+                break;
+            }
+            if (lds_acquire(&S.pub[slot]) != j) break;  // the parser ended before batch j
+            st.add(kStamps, kSsBatches, 1);
+            Batch bt;
+            bt.ls = S.rec[slot][0][lane];
+            bt.L = S.rec[slot][1][lane];
+            bt.op = S.rec[slot][2][lane];
+            bt.off = S.rec[slot][3][lane];
+            bt.M = S.rec[slot][4][lane];
+            int32_t hdr[kSWords];
+#pragma unroll
+            for (uint32_t q = 0; q < kSWords; ++q) hdr[q] = (int32_t)uni((uint32_t)S.hdr[slot][q]);
+            bt.n = (uint32_t)hdr[kSN];
+            if (hdr[kSKind] == kKindHbm) {
+                lds_release(&S.con[slot], j);
+                ps.flush(gout);
+                copy_scalar_hbm<4>(bt, in, srcSize, gout, outSize, lane, [&] {
+                    if (lane == 0)
+                        __hip_atomic_fetch_add(&S.beat, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                });
+                stream_refill(S, hdr[kSLo], hdr[kSHi], gout, lane);
+                st.lap(kStamps, kSsScalar);
+            } else {
+                stream_fast<kStamps>(S, slot, bt, hdr[kSLo], hdr[kSHi], hdr[kSBase], gout, lane, ps, st);
+                lds_release(&S.con[slot], j);
+                st.lap(kStamps, kSsFast);
+            }
+        }
+        ps.flush(gout);
+    }
+    __syncthreads();
+    if (tid == 0) ret[b] = __hip_atomic_load(&S.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                               ? kPipeAbort
+                               : S.result;
+    if constexpr (kStamps) {
+        if (lane == 0 && dbg) {
+            uint64_t* d = dbg + kStSlots * (size_t)b;
+            for (int k = 0; k < kSsSlots; ++k)
+                if (st.a[k]) atomicAdd((unsigned long long*)(d + k), (unsigned long long)st.a[k]);
+        }
+    }
+}
+
 // Blocks whose capacity is at least this take the pipelined decoder (small
 // blocks parse in a few batches; one wave each keeps more of them resident).
 constexpr uint32_t kPipeMinCap = 16384;
@@ -1521,6 +1919,7 @@ constexpr uint32_t kPipeMinCap = 16384;
 // their capacity (stored / incompressible data: a few long literal runs) are
 // the lightest.
 constexpr uint32_t kOrderMin = 256 * (24 / kPipeWaves);  // one round of pipelined workgroups
+constexpr uint32_t kStreamOrderMin = 256 * 2 * LZ4E_STREAM_WAVES_PER_EU;  // one round of streaming ones
 struct DecodeWeight {
     const int32_t* src_len;
     const int32_t* dst_cap;
@@ -1538,8 +1937,27 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
     // LZ4E_DECOMPRESS_MODE=wave|pipe overrides the choice (A/B experiments).
     static const char* env = getenv("LZ4E_DECOMPRESS_MODE");
     uint32_t mode = a.mode;
-    if (mode == kDecAuto && env) mode = env[0] == 'w' ? kDecWave : (env[0] == 'p' ? kDecPipe : kDecAuto);
+    if (mode == kDecAuto && env)
+        mode = env[0] == 'w' ? kDecWave : (env[0] == 'p' ? kDecPipe : (env[0] == 's' ? kDecStream : kDecAuto));
     if (mode == kDecAuto) mode = (a.max_cap == 0 || a.max_cap >= kPipeMinCap) ? kDecPipe : kDecWave;
+    if (mode == kDecStream) {
+        const int om = launch_order_mode(false);
+        uint32_t* order = nullptr;
+        if ((om == kOrderAlways || (om == kOrderAuto && a.nblocks > kStreamOrderMin)) &&
+            hipMallocAsync((void**)&order, sizeof(uint32_t) * a.nblocks, stream) == hipSuccess) {
+            hipLaunchKernelGGL((order_kernel<DecodeWeight>), dim3(1), dim3(kOrderThreads), 0, stream,
+                               DecodeWeight{a.src_len, a.dst_cap}, a.nblocks, order);
+        } else {
+            (void)hipGetLastError();
+            order = nullptr;
+        }
+        hipLaunchKernelGGL((decompress_stream_kernel<kStamps>), dim3(a.nblocks), dim3(2 * kWave), 0,
+                           stream, a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret,
+                           a.nblocks, dbg, a.dict_len, (const uint32_t*)order);
+        const hipError_t err = hipGetLastError();
+        if (order) (void)hipFreeAsync(order, stream);
+        return err;
+    }
     if (mode == kDecPipe) {
         const int om = launch_order_mode(false);
         uint32_t* order = nullptr;

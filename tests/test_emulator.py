@@ -233,13 +233,13 @@ def test_emulated_decoder_vector_extension_truncated_in_run(emu_exe_vecext, tmp_
 # atomics) on the emulator, under the same sanitizers.
 # ---------------------------------------------------------------------------
 
-def _emu_decode_pipe(exe, tmp_path, frame, cap, dic=b""):
+def _emu_decode_pipe(exe, tmp_path, frame, cap, dic=b"", flag="-p"):
     f, o, d = tmp_path / "f.bin", tmp_path / "o.bin", tmp_path / "d.bin"
     f.write_bytes(frame)
     d.write_bytes(dic)
     if o.exists():
         o.unlink()
-    out = subprocess.run([exe, "-p", str(f), str(cap), str(o), str(d)], capture_output=True, text=True,
+    out = subprocess.run([exe, flag, str(f), str(cap), str(o), str(d)], capture_output=True, text=True,
                          timeout=600)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "ERROR: AddressSanitizer" not in out.stderr and "runtime error" not in out.stderr
@@ -251,12 +251,14 @@ def _emu_decode_pipe(exe, tmp_path, frame, cap, dic=b""):
 PIPE_CASES = [(k, m) for k in ("text", "records", "ints", "runs") for m in range(5)] + [("random", 0)]
 
 
+@pytest.mark.parametrize("flag", ["-p", "-s"], ids=["pipe", "stream"])
 @pytest.mark.parametrize("kind,mode", PIPE_CASES, ids=[f"{k}-{m}" for k, m in PIPE_CASES])
-def test_emulated_pipe_decoder_sanitized(emu_exe, tmp_path, kind, mode):
-    """The 4-wave pipelined decoder on 16-64 KiB blocks: valid frames (mode
-    0), truncations (1), bit flips (2), short capacity (3) and a dictionary
-    (4): values, error codes and bytes equal the oracle's
-    (/root/reference/lz4e/lz4e_decompress.c:62-460 restated)."""
+def test_emulated_pipe_decoder_sanitized(emu_exe, tmp_path, kind, mode, flag):
+    """The 4-wave pipelined decoder (-p) and the 2-wave streaming decoder (-s)
+    on 16-64 KiB blocks: valid frames (mode 0), truncations (1), bit flips
+    (2), short capacity (3) and a dictionary (4): values, error codes and
+    bytes equal the oracle's (/root/reference/lz4e/lz4e_decompress.c:62-460
+    restated)."""
     rng = np.random.default_rng(700 + mode + 17 * len(kind))
     n = int(rng.integers(16384, 65536))
     data = _block(kind, n + 9000, 31 + n).tobytes()
@@ -273,7 +275,7 @@ def test_emulated_pipe_decoder_sanitized(emu_exe, tmp_path, kind, mode):
     elif mode == 3:
         cap = max(0, cap - int(rng.integers(1, 40)))
     want = oracle_ref.decompress_dict(f, cap, dic)
-    got = _emu_decode_pipe(emu_exe, tmp_path, f, cap, dic)
+    got = _emu_decode_pipe(emu_exe, tmp_path, f, cap, dic, flag)
     assert got[0] == want[0], (got[0], want[0])
     if want[0] >= 0:
         assert got[1] == want[1]
@@ -288,7 +290,8 @@ def emu_exe_spin1(tmp_path_factory):
     shutil.rmtree(b, ignore_errors=True)
 
 
-def test_emulated_pipe_decoder_watchdog(emu_exe_spin1, tmp_path):
+@pytest.mark.parametrize("flag", ["-p", "-s"], ids=["pipe", "stream"])
+def test_emulated_pipe_decoder_watchdog(emu_exe_spin1, tmp_path, flag):
     """A forced watchdog: every wave leaves its loop (the run ends), the
     block's value is LZ4E_DECODE_ABORTED -- even though the parser itself
     finished the parse -- and the host's reading of the batch
@@ -296,7 +299,7 @@ def test_emulated_pipe_decoder_watchdog(emu_exe_spin1, tmp_path):
     with the watchdog named in lz4e_last_error's text."""
     blk = _block("text", 65536, 9).tobytes()
     f = oracle_ref.compress(blk, BYU16)[1]
-    r, _, res = _emu_decode_pipe(emu_exe_spin1, tmp_path, f, len(blk))
+    r, _, res = _emu_decode_pipe(emu_exe_spin1, tmp_path, f, len(blk), flag=flag)
     assert r == -2**31
     good, msg = res.split(" ", 2)[1:]
     assert int(good) == -1 and "watchdog" in msg and "LZ4E_DECODE_ABORTED" in msg
