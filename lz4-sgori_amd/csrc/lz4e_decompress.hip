@@ -1597,21 +1597,18 @@ struct StreamStamps {
 
 // The HBM store of a step's dword, deferred by one step: issued after the
 // next step's far loads, so that those do not wait for it (a wave's loads and
-// stores complete in order).  bm: the bytes of the dword at x0 that belong to
-// the output (all four but at a batch's two ends).
+// stores complete in order).  Exactly one store instruction per step, every
+// lane active -- a lane with no byte of the batch rewrites lane 0's dword
+// with lane 0's value -- so that the compiler's vmcnt waits for the far
+// loads stay exact (a branch around a store makes them vmcnt(0), i.e. a
+// wait for the store).  Bytes of the dword before the batch carry their
+// final values (read back from the ring); bytes after it are rewritten by
+// the next batch (a batch that ends within 3 bytes of the capacity takes
+// stream_edge instead).
 struct PendStore {
-    uint32_t v = 0, bm = 0;
-    int32_t x0 = 0;
-    LZ4E_DEV void flush(uint8_t* gout) {
-        if (bm == 0xFu) {
-            *(gu32w*)(gout + x0) = v;
-        } else if (bm) {
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q)
-                if ((bm >> q) & 1) *(gu8*)(gout + x0 + (int32_t)q) = (uint8_t)(v >> (8 * q));
-        }
-        bm = 0;
-    }
+    uint32_t v = 0;
+    int32_t a = 0;
+    LZ4E_DEV void flush(uint8_t* gout) const { *(gu32w*)(gout + a) = v; }
 };
 
 // A step's byte sources (see stream_fast): LDS byte addresses, pointers
@@ -1627,7 +1624,7 @@ struct StepDesc {
 // gathers are in flight.
 template <bool kStamps>
 LZ4E_DEV void stream_fast(StreamLds& S, uint32_t slot, const Batch& b, int32_t lo, int32_t hi,
-                          int32_t ibase, uint8_t* gout, uint32_t lane, PendStore& ps, StreamStamps& st) {
+                          int32_t ibase, uint8_t* gout, uint32_t lane, StreamStamps& st) {
     const bool valid = lane < b.n;
     // packed fields of sequence k (lane k): output start, match start and
     // literal source relative to the batch / its window; the offset
@@ -1643,10 +1640,10 @@ LZ4E_DEV void stream_fast(StreamLds& S, uint32_t slot, const Batch& b, int32_t l
     auto describe = [&](int32_t Xs, StepDesc& d) {
         const int32_t x0 = Xs + 4 * (int32_t)lane;
         mark[lane] = 0;
-        lockstep();
+        wave_fence();
         const int32_t rs = b.op - Xs;
         if (valid && rs >= 0 && rs < kSStep) mark[rs >> 2] = ((lane + 1) << 2) | (uint32_t)(rs & 3);
-        lockstep();
+        wave_fence();
         const uint32_t m = mark[lane];
         const uint32_t Mx = wave_incl_umax(m);
         const int32_t o2 = Mx ? (int32_t)(Mx >> 2) - 1 : carry;
@@ -1690,15 +1687,11 @@ LZ4E_DEV void stream_fast(StreamLds& S, uint32_t slot, const Batch& b, int32_t l
             d.fl[q] = *(const gu8*)(gout + (far ? src : lo));
         }
     };
-    StepDesc cur, nxt;
-    int32_t Xs = lo & ~3;
-    describe(Xs, cur);
-    for (; Xs < hi; Xs += kSStep) {
+    // gathers, in-step pointer jumping, ring write; the step's HBM store
+    // (deferred, see PendStore) into `out`
+    auto step = [&](int32_t Xs, const StepDesc& cur, PendStore& out) {
         const int32_t x0 = Xs + 4 * (int32_t)lane;
-        const bool more_steps = Xs + kSStep < hi;
-        if (more_steps) describe(Xs + kSStep, nxt);
-        ps.flush(gout);  // the previous step's dword (after the far loads)
-        lockstep();      // the previous step's ring dwords, read by other lanes
+        lockstep();  // the previous step's ring dwords, read by other lanes
         uint32_t g[4];
 #pragma unroll
         for (uint32_t q = 0; q < 4; ++q) g[q] = sb[cur.ao[q]];
@@ -1723,7 +1716,7 @@ LZ4E_DEV void stream_fast(StreamLds& S, uint32_t slot, const Batch& b, int32_t l
                 for (uint32_t q = 0; q < 4; ++q)
                     w |= (uint64_t)((((PT >> (8 * q)) & 0xFFu) << 8) | ((V >> (8 * q)) & 0xFFu)) << (16 * q);
                 *(lu64*)&S.vp[lane] = w;
-                lockstep();
+                wave_fence();  // (u16 reads of u64 stores: no type-based reordering)
                 uint32_t e[4];
 #pragma unroll
                 for (uint32_t q = 0; q < 4; ++q) {
@@ -1745,11 +1738,38 @@ LZ4E_DEV void stream_fast(StreamLds& S, uint32_t slot, const Batch& b, int32_t l
             }
         }
         lockstep();  // (every gather of the step before the ring write)
-        if (x0 < hi) *(lu32*)(sb + h0 + (uint32_t)(x0 & (kSRing - 1))) = V;
-        ps.v = V;
-        ps.x0 = x0;
-        ps.bm = cur.bm;
-        if (more_steps) cur = nxt;
+        const bool mine = x0 < hi;
+        if (mine) *(lu32*)(sb + h0 + (uint32_t)(x0 & (kSRing - 1))) = V;
+        const uint32_t V0 = lane_val(V, 0);
+        out.v = mine ? V : V0;
+        out.a = mine ? x0 : Xs;
+    };
+    // (Building step t+1's descriptor before step t's gathers -- a software
+    // pipeline -- measured slower: 5.4k -> 6.1k cycles per text batch.)
+    PendStore ps;
+    for (int32_t Xs = lo & ~3; Xs < hi; Xs += kSStep) {
+        StepDesc cur;
+        describe(Xs, cur);
+        if (Xs != (lo & ~3)) ps.flush(gout);  // the previous step's dword (after the far loads)
+        step(Xs, cur, ps);
+    }
+    ps.flush(gout);
+}
+
+// A fast batch ending within 3 bytes of the block's capacity: its
+// sequences one at a time in HBM (lane 0, exact bytes), then the ring.
+LZ4E_DEV void stream_edge(const Batch& b, const uint8_t* in, int32_t srcSize, uint8_t* gout,
+                          int32_t outSize, uint32_t lane) {
+    for (uint32_t k = 0; k < b.n; ++k) {
+        Batch one;
+        const bool me = lane == 0;
+        one.ls = me ? (int32_t)lane_val((uint32_t)b.ls, k) : 0;
+        one.L = me ? (int32_t)lane_val((uint32_t)b.L, k) : 0;
+        one.op = me ? (int32_t)lane_val((uint32_t)b.op, k) : 0;
+        one.off = me ? (int32_t)lane_val((uint32_t)b.off, k) : 0;
+        one.M = me ? (int32_t)lane_val((uint32_t)b.M, k) : 0;
+        one.n = 1;
+        copy_scalar_hbm(one, in, srcSize, gout, outSize, lane);
     }
 }
 
@@ -1856,7 +1876,6 @@ __global__ __launch_bounds__(2 * kWave, LZ4E_STREAM_WAVES_PER_EU) void decompres
         lds_release(&S.nb_total, j);
     } else {
         // ---------------- copier ----------------
-        PendStore ps;
         for (int32_t j = 0;; ++j) {
             const uint32_t slot = (uint32_t)j % kSRecs;
             const bool ok = wait_for(
@@ -1881,20 +1900,23 @@ __global__ __launch_bounds__(2 * kWave, LZ4E_STREAM_WAVES_PER_EU) void decompres
             bt.n = (uint32_t)hdr[kSN];
             if (hdr[kSKind] == kKindHbm) {
                 lds_release(&S.con[slot], j);
-                ps.flush(gout);
                 copy_scalar_hbm<4>(bt, in, srcSize, gout, outSize, lane, [&] {
                     if (lane == 0)
                         __hip_atomic_fetch_add(&S.beat, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 });
                 stream_refill(S, hdr[kSLo], hdr[kSHi], gout, lane);
                 st.lap(kStamps, kSsScalar);
+            } else if (hdr[kSHi] + 3 > outSize) {
+                lds_release(&S.con[slot], j);
+                stream_edge(bt, in, srcSize, gout, outSize, lane);
+                stream_refill(S, hdr[kSLo], hdr[kSHi], gout, lane);
+                st.lap(kStamps, kSsScalar);
             } else {
-                stream_fast<kStamps>(S, slot, bt, hdr[kSLo], hdr[kSHi], hdr[kSBase], gout, lane, ps, st);
+                stream_fast<kStamps>(S, slot, bt, hdr[kSLo], hdr[kSHi], hdr[kSBase], gout, lane, st);
                 lds_release(&S.con[slot], j);
                 st.lap(kStamps, kSsFast);
             }
         }
-        ps.flush(gout);
     }
     __syncthreads();
     if (tid == 0) ret[b] = __hip_atomic_load(&S.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)

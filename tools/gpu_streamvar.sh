@@ -7,6 +7,6 @@ cp $so /tmp/orig.so
 for v in lz4-sgori_amd/build/var/lib*.so; do
   cp $v $so
   echo "## $v"
-  timeout -k 10 300 python -u tools/streamab.py ${SV_NB:-256} ${SV_KINDS:-text,ints,records} 2>&1 | grep -v amdgpu.ids || exit 1
+  timeout -k 10 300 python -u tools/streamab.py ${SV_NB:-256} ${SV_KINDS:-text,ints,records} 2>&1 | grep -v amdgpu.ids
 done
 cp /tmp/orig.so $so
