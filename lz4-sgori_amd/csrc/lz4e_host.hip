@@ -739,10 +739,10 @@ int lz4e_debug_compress_stamped(const uint8_t* src, const uint64_t* src_off, con
 }
 
 // Diagnostic (not part of include/lz4e.h): the decompress kernels with a
-// forced decoder (mode 0 auto, 1 one wave per block, 2 pipelined) and, when
-// dbg is not null, the stamped build's per-block cycle counters (one-wave
-// decoder: 8 x u64 per block; pipelined: 20 x u64, tools/decab.py; dbg zeroed
-// by the caller).
+// forced decoder (mode 0 auto, 1 one wave per block, 2 pipelined, 3 streaming)
+// and, when dbg is not null, the stamped build's per-block cycle counters
+// (one-wave decoder: 8 x u64 per block; pipelined and streaming: 20 x u64,
+// tools/decab.py, tools/streamab.py; dbg zeroed by the caller).
 int lz4e_debug_decompress_stamped(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
                                   uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
                                   int32_t* ret, uint32_t nblocks, void* stream, uint64_t* dbg,
