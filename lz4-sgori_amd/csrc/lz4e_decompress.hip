@@ -1829,7 +1829,9 @@ __global__ __launch_bounds__(2 * kWave, LZ4E_STREAM_WAVES_PER_EU) void decompres
 
     if (wave == 0) {
         // ---------------- parser (as in decompress_pipe_kernel) ----------------
-        __builtin_amdgcn_s_setprio(3);
+        // (issue priority: the copier is this kernel's critical path; parser
+        // 1 / copier 3 measured 0.95 -> 0.90 ms on silesia64k against 3 / 0)
+        __builtin_amdgcn_s_setprio(1);
         Parse P;
         P.init(in, srcSize, outSize, (lu32*)S.ring, lane, dict_of(dict_len, b));
         int32_t j = 0;
@@ -1876,6 +1878,7 @@ __global__ __launch_bounds__(2 * kWave, LZ4E_STREAM_WAVES_PER_EU) void decompres
         lds_release(&S.nb_total, j);
     } else {
         // ---------------- copier ----------------
+        __builtin_amdgcn_s_setprio(3);
         for (int32_t j = 0;; ++j) {
             const uint32_t slot = (uint32_t)j % kSRecs;
             const bool ok = wait_for(
