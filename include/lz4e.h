@@ -12,10 +12,15 @@
  * Both single-call entry points run on the GPU (gfx950): the host shim
  * gathers the bio_vec segments into pinned staging, copies them to HBM,
  * launches the hand-written HIP kernel and scatters the frame back into the
- * destination bio_vecs.  Like the reference they are reentrant: concurrent
- * callers each lease their own HIP stream and staging (no global lock).  There is no CPU codec behind these symbols; when no
- * GPU is usable they fail (compress returns 0, decompress returns a negative
- * value) and lz4e_last_error() says why.
+ * destination bio_vecs.  Like the reference they are reentrant.  Concurrent
+ * callers on one device are coalesced: a caller queues its request, and a
+ * caller that finds fewer than 4 batches in flight runs every queued
+ * request of that device (its own included) as one batch launch on its own
+ * thread and leased HIP stream while the others wait for their result; a
+ * lone caller runs at once.  A batch that fails as a whole is rerun call by
+ * call, so one caller's failure is not another's.  There is no CPU codec
+ * behind these symbols; when no GPU is usable they fail (compress returns
+ * 0, decompress returns a negative value) and lz4e_last_error() says why.
  *
  * The batched lz4e_*_batch_* entry points are the throughput path: many
  * independent blocks per launch, device-resident buffers, caller's stream.

@@ -59,10 +59,13 @@ constexpr uint32_t kSpan = 64 * 32 + 16 + 48;       // a fast batch's output, 16
 constexpr uint32_t kJump = 2 * kSpan;               // u16 per span byte (chain resolution)
 constexpr uint16_t kFinal = 0xFFFF;                 // jump entry of a byte whose value is final
 
+// LDS access types.  Every wider type may alias every other (may_alias):
+// the decoders read LDS bytes through whichever width suits the step, so no
+// access order may rest on type-based alias analysis.
 typedef __attribute__((address_space(3))) uint8_t lu8;
-typedef __attribute__((address_space(3))) uint32_t lu32;
-typedef __attribute__((address_space(3))) uint16_t lu16;
-typedef uint32_t __attribute__((aligned(1))) u32a1;
+typedef __attribute__((address_space(3), may_alias)) uint32_t lu32;
+typedef __attribute__((address_space(3), may_alias)) uint16_t lu16;
+typedef uint32_t __attribute__((aligned(1), may_alias)) u32a1;
 typedef __attribute__((address_space(3))) u32a1 lu32a1;
 
 LZ4E_DEV uint32_t ld4(const lu8* p) { return *(const lu32a1*)p; }
@@ -1090,11 +1093,11 @@ LZ4E_DEV void lds_release(int32_t* p, int32_t v) {
 }
 
 // u16 x 4 at a jump-table index (unaligned forms for the pointer runs).
-typedef uint64_t __attribute__((aligned(2))) u64a2;
+typedef uint64_t __attribute__((aligned(2), may_alias)) u64a2;
 typedef __attribute__((address_space(3))) u64a2 lu64a2;
-typedef __attribute__((address_space(3))) uint64_t lu64;
+typedef __attribute__((address_space(3), may_alias)) uint64_t lu64;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) u32x4 lu128;
+typedef __attribute__((address_space(3), may_alias)) u32x4 lu128;
 LZ4E_DEV int32_t wave_min_i32(int32_t v) {
     const int32_t e = wave_excl_min(v);
     const int32_t m = e < v ? e : v;
@@ -1934,6 +1937,624 @@ __global__ __launch_bounds__(2 * kWave, LZ4E_STREAM_WAVES_PER_EU) void decompres
     }
 }
 
+// ============================================================================
+// Chunked decoder: one wave per block, a token list per 1 KiB of input
+// ============================================================================
+//
+// The two decoders above find each batch's tokens by pointer doubling over a
+// 256-byte window (five table compositions and six lookups, all dependent
+// LDS round trips, ~3.6 k cycles for ~45 text sequences), and resolve copies
+// byte by byte.  This one finds the tokens of a whole 1 KiB chunk of the
+// compressed stream at once and copies whole sequences per lane:
+//
+//  * Input window: compressed bytes [wb, wb + 2 KiB) in LDS (the chunk and
+//    the next one: a token near the chunk's end reads ahead), loaded with
+//    range-checked dword buffer loads; the next 1 KiB is prefetched into
+//    registers while the chunk's batches run.
+//  * Token walk (ck_parse): lane l walks the token chain from the start of
+//    its 16-byte segment [16 l, 16 l + 16) of the chunk -- a speculative
+//    entry -- until the chain leaves the segment: token byte, up to 3
+//    extension bytes per length field (one unaligned dword read each),
+//    next = token + 1 + ext + L + 2 + ext.  LZ4 token chains started at
+//    different positions merge within a few tokens, so nearly every lane's
+//    walk passes through the true chain's first token in its segment; the
+//    lanes whose walk does not (checked against the true entry handed over
+//    from the lane before, one shuffle per round) walk again from it.  After
+//    at most 65 rounds (each fixes the next lane; in practice 1-3) every
+//    lane's tokens from its true entry on are the reference's, and a prefix
+//    sum packs them into a list (position | L << 11 | M << 22).  A token the
+//    walk cannot take (a length-extension run of more than 3 bytes, bytes
+//    past the window, a position past iend - 18) ends the chain: the exact
+//    path takes it.
+//  * Fast batches: up to 64 listed sequences, sequence k in lane k.  The
+//    reference's checks of the sequence (lz4e_decompress.c:150-191 for a
+//    token without extension bytes; :194-220, :223-296 and :298-336 with
+//    them) are evaluated per lane with bounds strong enough that every one
+//    of them passes -- a sequence that fails them, or the batch's 1 KiB
+//    output cap, ends the batch; the exact path (ck_exact: the reference's
+//    checks in its order, one sequence, copies in HBM) decides the rest.
+//  * Output window: output bytes [ob, ob + kCkOut) in LDS.  A batch's
+//    literals are copied from the input window, the part of each match
+//    whose source lies before the batch from the window (or from HBM when it
+//    lies before ob: the window is flushed 16 bytes per lane, in order, long
+//    before its bytes leave it), and the rest -- sources inside the batch --
+//    in readiness rounds (a match is ready when its source overlaps no
+//    earlier pending match) or by pointer jumping over the batch's span when
+//    few are ready (dependency chains: records, integer tables).
+//
+// One wave owns every byte of its block, so no wave waits for another: no
+// progress counters and no watchdog.  Offset 0 writes zeros, as in the other
+// decoders (lz4e_decompress.c:313, 407-415).
+#ifndef LZ4E_CK_OUT
+#define LZ4E_CK_OUT 8192
+#endif
+#ifndef LZ4E_CK_KEEP
+#define LZ4E_CK_KEEP 4096
+#endif
+constexpr int32_t kCkChunk = 1024;            // compressed bytes per chunk
+constexpr int32_t kCkSeg = 16;                // ... per lane
+constexpr int32_t kCkIn = 2 * kCkChunk;       // input window
+constexpr int32_t kCkSlots = 6;               // tokens per segment at most (3+ bytes each)
+constexpr int32_t kCkOut = LZ4E_CK_OUT;       // output window
+constexpr int32_t kCkKeep = LZ4E_CK_KEEP;     // history kept when the window moves
+constexpr int32_t kCkCap = 1024;              // output bytes per fast batch
+constexpr int32_t kCkFlush = 2048;            // flush lag
+static_assert(kCkKeep >= kCkFlush + 32 && kCkOut >= kCkKeep + 2 * kCkCap && kCkOut % 16 == 0,
+              "chunked decoder window sizes");
+
+struct CkLds {
+    uint8_t in[kCkIn + 16];               // input window (+ pad for reads at its end)
+    uint32_t tok[kWave * kCkSlots];       // walk slots, then the chunk's token list
+    uint8_t out[kCkOut + 16];             // output window
+    uint16_t jump[kCkCap + 32];           // pointer jumping over a batch's span
+    uint8_t sink[kSink];                  // a dword per lane for unwanted stores
+};
+
+// List entry: window position (11 bits), literal length (11), match length
+// incl. the 4 (10).
+LZ4E_DEV int32_t ck_pos(uint32_t e) { return (int32_t)(e & 2047u); }
+LZ4E_DEV int32_t ck_L(uint32_t e) { return (int32_t)((e >> 11) & 2047u); }
+LZ4E_DEV int32_t ck_M(uint32_t e) { return (int32_t)(e >> 22); }
+// Extension bytes of a length field of value v (>= 15: 15 + 255 (k - 1) + last, last < 255).
+LZ4E_DEV int32_t ck_ext(int32_t v) { return v < 15 ? 0 : (v < 270 ? 1 : (v < 525 ? 2 : 3)); }
+
+// Extension run at p (dword e = bytes p..p+3): run length k (1..3; 0: longer)
+// and the field's value.
+LZ4E_DEV uint32_t ck_run(uint32_t e, uint32_t& v) {
+    const uint32_t k = (e & 0xFFu) != 0xFFu ? 1u : (((e >> 8) & 0xFFu) != 0xFFu ? 2u : (((e >> 16) & 0xFFu) != 0xFFu ? 3u : 0u));
+    const uint32_t kk = k ? k : 1u;
+    v = 15u + 255u * (kk - 1u) + ((e >> (8 * (kk - 1u))) & 0xFFu);
+    return k;
+}
+
+// One token at window position p: its list entry and the position of the
+// token after it; false when the walk cannot take it (an extension run of
+// more than 3 bytes, or bytes read past the window).
+LZ4E_DEV bool ck_token(const lu8* in, int32_t p, uint32_t& entry, int32_t& next) {
+    const uint32_t t = in[p];
+    uint32_t L = t >> 4, Mt = t & 15u;
+    int32_t q = p + 1;
+    bool ok = true;
+    if (L == 15) {
+        const uint32_t k = ck_run(ld4(in + q), L);
+        ok = k != 0;
+        q += (int32_t)k;
+    }
+    int32_t nx = q + (int32_t)L + 2;
+    if (ok && Mt == 15) {
+        if (nx + 4 > kCkIn) {
+            ok = false;
+        } else {
+            const uint32_t k = ck_run(ld4(in + nx), Mt);
+            ok = k != 0;
+            nx += (int32_t)k;
+        }
+    }
+    ok = ok && nx + 4 <= kCkIn;
+    entry = (uint32_t)p | (L << 11) | ((Mt + 4u) << 22);
+    next = nx;
+    return ok;
+}
+
+// The chain from p while it stays inside the segment [ss, se): every token
+// walked gets a visit bit and a slot; x is the first position at or past se,
+// or the token the walk could not take (stp).
+struct CkWalk {
+    uint32_t vis = 0, cnt = 0;
+    int32_t x = 0;
+    bool stp = false;
+};
+LZ4E_DEV CkWalk ck_walk(const lu8* in, lu32* slot, int32_t p, int32_t ss, int32_t se, int32_t plim) {
+    CkWalk w;
+    while (p < se) {  // at most kCkSlots tokens
+        uint32_t e;
+        int32_t nx;
+        if (p > plim || !ck_token(in, p, e, nx)) {
+            w.stp = true;
+            break;
+        }
+        w.vis |= 1u << (p - ss);
+        slot[w.cnt++] = e;
+        p = nx;
+    }
+    w.x = p;
+    return w;
+}
+
+// The chunk's tokens from the true entry E (window position in [0, kCkChunk)):
+// the list in S.tok[0, n), the chain's exit x (first position past the
+// chunk, or the token the walk could not take: stp).
+struct CkList {
+    int32_t n = 0, x = 0;
+    bool stp = false;
+};
+LZ4E_DEV CkList ck_parse(CkLds& S, int32_t E, int32_t plim, uint32_t lane) {
+    const int32_t ss = kCkSeg * (int32_t)lane, se = ss + kCkSeg;
+    const uint32_t l0 = (uint32_t)E >> 4;
+    const bool act = lane >= l0;
+    const lu8* in = (const lu8*)S.in;
+    lu32* slot = (lu32*)S.tok + kCkSlots * lane;
+    int32_t T = lane == l0 ? E : ss;  // assumed first token of the true chain in the segment
+    int32_t st = T;                   // where this lane's walk started
+    bool sf = false;                  // the true chain stopped before this segment
+    CkWalk w;
+    w.x = se;
+    if (act) w = ck_walk(in, slot, T, ss, se, plim);
+    bool settled = false;
+    for (uint32_t it = 0; it < kWave + 2; ++it) {
+        // hand-over from the lane before: its true chain's first position in this segment
+        const int32_t pT = shfl_up(T, 1), px = shfl_up(w.x, 1);
+        const int32_t pf = shfl_up((sf ? 1 : 0) | (w.stp ? 2 : 0), 1);
+        int32_t nT = T;
+        bool nsf = sf;
+        if (lane > l0) {
+            if (pf & 1) {
+                nT = pT;
+                nsf = true;
+            } else if (pT >= ss) {  // the chain passed over the lane before
+                nT = pT;
+                nsf = false;
+            } else {
+                nT = px;
+                nsf = (pf & 2) != 0;
+            }
+        }
+        const bool cons = !act || nsf || nT >= se ||
+                          (nT >= st && ((w.vis >> (nT - ss)) & 1u)) || (w.stp && w.x == nT);
+        const bool chg = nT != T || nsf != sf;
+        if (!ballot(!cons || chg)) {
+            settled = true;
+            break;
+        }
+        T = nT;
+        sf = nsf;
+        if (!cons) {
+            st = T;
+            w = ck_walk(in, slot, T, ss, se, plim);
+        }
+    }
+    CkList r;
+    if (!settled) {  // (cannot happen: each round settles the next lane) -- the exact path decides
+        r.n = 0;
+        r.x = E;
+        r.stp = true;
+        return r;
+    }
+    // this lane's true tokens: its slots from T on
+    uint32_t j0 = 0, nt = 0;
+    if (act && !sf && T < se) {
+        j0 = popc64(w.vis & ((1u << (T - ss)) - 1u));
+        nt = w.cnt - j0;
+    }
+    const uint32_t incl = wave_incl_add(nt);
+    const uint32_t base = incl - nt;
+    uint32_t e[kCkSlots];
+#pragma unroll
+    for (uint32_t q = 0; q < kCkSlots; ++q) e[q] = q < nt ? slot[j0 + q] : 0u;
+    lockstep();  // every lane has read its slots before the list overwrites them
+    lu32* list = (lu32*)S.tok;
+#pragma unroll
+    for (uint32_t q = 0; q < kCkSlots; ++q)
+        if (q < nt) list[base + q] = e[q];
+    lockstep();
+    r.n = (int32_t)lane_val(incl, kWave - 1);
+    // the exit: what lane 63 hands over
+    const int32_t T63 = (int32_t)lane_val((uint32_t)T, kWave - 1);
+    const int32_t x63 = (int32_t)lane_val((uint32_t)w.x, kWave - 1);
+    const uint32_t f63 = lane_val((sf ? 1u : 0u) | (w.stp ? 2u : 0u), kWave - 1);
+    if (f63 & 1u) {
+        r.x = T63;
+        r.stp = true;
+    } else if (T63 >= kWave * kCkSeg) {
+        r.x = T63;
+        r.stp = false;
+    } else {
+        r.x = x63;
+        r.stp = (f63 & 2u) != 0;
+    }
+    return r;
+}
+
+// Byte p of the block from HBM (the exact path reads the input there).
+LZ4E_DEV uint32_t ck_gbyte(const ByteBuf& ib, int32_t sh, int32_t p) {
+    const uint32_t q = vaddr((uint32_t)(p + sh));
+    return uni((buf_ld32(ib, q & ~3u) >> (8 * (q & 3u))) & 0xFFu);
+}
+// Length-extension scan in HBM, 256 bytes per step: the first position q >=
+// p0 whose byte is not 255 or that is >= plim (p0 <= plim).
+LZ4E_DEV int32_t ck_ext_stop(const ByteBuf& ib, int32_t sh, int32_t p0, int32_t plim, uint32_t lane) {
+    for (int32_t b = (p0 + sh) & ~3;; b += 4 * (int32_t)kWave) {
+        const int32_t qa = b + 4 * (int32_t)lane;
+        const uint32_t w = buf_ld32(ib, vaddr((uint32_t)qa));
+        uint32_t m = 0;
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t) {
+            const int32_t q = qa + (int32_t)t - sh;
+            const bool stop = q >= p0 && (((w >> (8 * t)) & 0xFFu) != 0xFFu || q >= plim);
+            m |= (stop ? 1u : 0u) << t;
+        }
+        const uint64_t bm = ballot(m != 0);
+        if (bm) {
+            const uint32_t l = ctz64(bm);
+            return b + 4 * (int32_t)l + (int32_t)__builtin_ctz(lane_val(m, l)) - sh;
+        }
+    }
+}
+
+// The exact path: one sequence at ip with every check of the reference in
+// its order (lz4e_decompress.c:123-446; the same decisions as parse_batch's
+// scalar path), its copies in HBM.  Returns kParsedScalar (ip / op past the
+// sequence; P.done for the final literal run) or kParseFail (ip: the
+// reference's failing position).
+LZ4E_DEV ParseResult ck_exact(const ByteBuf& ib, int32_t sh, const uint8_t* in, int32_t& ipr, int32_t& opr,
+                              int32_t iend, int32_t oend, int32_t D, bool& done, uint8_t* gout,
+                              uint32_t lane) {
+    int32_t ip = ipr, op = opr;
+    const int32_t shortiend = iend - 14 - 2, shortoend = oend - 14 - 18;  // :100-103
+    const uint32_t token = ck_gbyte(ib, sh, ip);
+    ip++;
+    uint32_t length = token >> 4;
+    int32_t offset = 0, lit_ip, lit_op;
+    uint32_t L;
+    if (length != 15 && ip < shortiend && op <= shortoend) {
+        // two-stage shortcut (:150-191)
+        lit_ip = ip;
+        lit_op = op;
+        L = length;
+        offset = (int32_t)(ck_gbyte(ib, sh, ip + (int32_t)length) |
+                           (ck_gbyte(ib, sh, ip + (int32_t)length + 1) << 8));
+        op += (int32_t)length;
+        ip += (int32_t)length + 2;
+        length = token & 15;
+        if (length != 15 && offset >= 8 && op >= offset) {
+            length += 4;  // 18-byte shortcut copy
+            goto record;
+        }
+        goto copy_match_checks;
+    }
+    if (length == 15) {  // :194-220
+        if (ip >= iend - 15) goto fail;
+        const int32_t q = ck_ext_stop(ib, sh, ip, iend - 16, lane);
+        const uint64_t sum = (uint64_t)length + 255ull * (uint64_t)(q - ip) + ck_gbyte(ib, sh, q);
+        length = sum > kSat ? kSat : (uint32_t)sum;
+        ip = q + 1;
+    }
+    {
+        const uint32_t cpy = (uint32_t)op + length;  // :223-288
+        const uint32_t iln = (uint32_t)ip + length;
+        lit_ip = ip;
+        lit_op = op;
+        L = length;
+        if (ugt(cpy, oend - 12) || ugt(iln, iend - 8)) {
+            if (iln != (uint32_t)iend || ugt(cpy, oend)) goto fail;
+            ip += (int32_t)length;
+            op += (int32_t)length;
+            length = 0;
+            done = true;  // final literal run: no match
+            goto record;
+        }
+        ip += (int32_t)length;
+        op = (int32_t)cpy;
+    }
+    offset = (int32_t)(ck_gbyte(ib, sh, ip) | (ck_gbyte(ib, sh, ip + 1) << 8));  // :291-296
+    ip += 2;
+    length = token & 15;
+copy_match_checks:
+    if (op - offset + D < 0) goto fail;  // :299-302
+    if (length == 15) {
+        const int32_t q = ck_ext_stop(ib, sh, ip, iend - 5, lane);
+        if (q + 1 > iend - 5) {
+            ip = q + 1;
+            goto fail;
+        }
+        const uint64_t sum = (uint64_t)length + 255ull * (uint64_t)(q - ip) + ck_gbyte(ib, sh, q);
+        length = sum > kSat ? kSat : (uint32_t)sum;
+        ip = q + 1;
+    }
+    if (ugt((uint32_t)op + length + 4, oend - 5)) goto fail;
+    length += 4;
+record:
+    {
+        Batch b;
+        const bool me = lane == 0;
+        b.ls = me ? lit_ip : 0;
+        b.L = me ? (int32_t)L : 0;
+        b.op = me ? lit_op : 0;
+        b.off = me ? offset : 0;
+        b.M = me ? (int32_t)length : 0;
+        b.n = 1;
+        copy_scalar_hbm<4>(b, in, iend, gout, oend, lane);
+    }
+    ipr = ip;
+    opr = op + (int32_t)length;
+    return kParsedScalar;
+fail:
+    ipr = ip;
+    return kParseFail;
+}
+
+// Block state of the chunked decoder (wave-uniform).
+struct CkState {
+    int32_t wb, ob, fl, op;  // input window base, output window base, flushed prefix, output position
+};
+
+// Store output [fl, to) (to a multiple of 16, or exact when tail) from the window.
+LZ4E_DEV void ck_flush(CkLds& S, uint8_t* gout, CkState& C, int32_t to, bool tail, uint32_t lane) {
+    const lu8* W = (const lu8*)S.out;
+    const int32_t t16 = to & ~15;
+    for (int32_t x = C.fl + 16 * (int32_t)lane; x < t16; x += 16 * (int32_t)kWave) {
+        const u32x4 v = *(const lu128*)(W + (x - C.ob));
+        stg16(gout + x, make_uint4(v.x, v.y, v.z, v.w));
+    }
+    if (tail && (int32_t)lane < to - t16 && t16 >= C.fl) *(gu8*)(gout + t16 + lane) = W[t16 - C.ob + lane];
+    C.fl = tail ? to : (t16 > C.fl ? t16 : C.fl);
+}
+
+// Moves the output window forward (keeps the last kCkKeep bytes).
+LZ4E_DEV void ck_slide(CkLds& S, CkState& C, uint32_t lane) {
+    int32_t nob = (C.op - kCkKeep) & ~15;
+    nob = nob < C.fl ? nob : (C.fl & ~15);
+    if (nob <= C.ob) return;
+    lu8* W = (lu8*)S.out;
+    const int32_t d = nob - C.ob, end = (C.op + 15) & ~15;
+    // forward in 1 KiB steps: step s writes [1024 s, +1024), reads d bytes
+    // further on -- never a range an earlier step wrote
+    for (int32_t x0 = 0; nob + x0 < end; x0 += 16 * (int32_t)kWave) {
+        const int32_t x = x0 + 16 * (int32_t)lane;
+        const bool act = nob + x < end;
+        u32x4 v = {0, 0, 0, 0};
+        if (act) v = *(const lu128*)(W + d + x);
+        lockstep();
+        if (act) *(lu128*)(W + x) = v;
+    }
+    lockstep();
+    C.ob = nob;
+}
+
+// One fast batch from list entry i (of n); returns the sequences decoded
+// (0: entry i takes the exact path).
+LZ4E_DEV uint32_t ck_batch(CkLds& S, CkState& C, int32_t i, int32_t n, int32_t iend, int32_t oend,
+                           int32_t D, uint8_t* gout, uint32_t lane) {
+    const lu8* in = (const lu8*)S.in;
+    lu8* W = (lu8*)S.out;
+    lu8* sink = (lu8*)S.sink + 4 * lane;
+    const int32_t idx = i + (int32_t)lane;
+    const bool have = idx < n;
+    const uint32_t e = have ? ((const lu32*)S.tok)[idx] : 0u;
+    const int32_t p = ck_pos(e), L = ck_L(e), M = ck_M(e);
+    const int32_t lp = p + 1 + ck_ext(L);
+    const int32_t off = have ? (int32_t)(ld4(in + lp + L) & 0xFFFFu) : 0;
+    const int32_t nx = lp + L + 2 + ck_ext(M - 4);
+    const int32_t size = have ? L + M : 0;
+    const int32_t incl = (int32_t)wave_incl_add((uint32_t)size);
+    const int32_t op = C.op;
+    const int32_t o = op + incl - size, m = o + L;
+    const bool ext = L >= 15 || M >= 19;
+    // every check of the reference on this sequence passes (header comment)
+    bool fast;
+    if (ext)
+        fast = C.wb + nx <= iend - 17 && o + size <= oend - 32 && m - off + D >= 0;
+    else
+        fast = C.wb + p <= iend - 18 && o <= oend - 32 &&
+               (m >= off ? (off >= 8 || m + M <= oend - 5) : (m - off + D >= 0 && m + M <= oend - 5));
+    const bool ok = have && fast && incl <= kCkCap;
+    const uint64_t okm = ballot(ok);
+    const uint32_t nf = (~okm) ? ctz64(~okm) : kWave;
+    if (nf == 0) return 0;
+    const bool valid = lane < nf;
+    const int32_t lo = op, hi = op + (int32_t)lane_val((uint32_t)incl, nf - 1);
+    const int32_t ob = C.ob;
+    // the part of the match whose source lies before the batch: final, from
+    // the window, or from HBM before ob (flushed: ob <= fl)
+    const int32_t ss = m - off;
+    int32_t n0 = 0, nh = 0;
+    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0;
+    if (valid && off != 0 && ss < lo) {
+        n0 = M < lo - ss ? M : lo - ss;
+        nh = ss < ob ? (n0 < ob - ss ? n0 : ob - ss) : 0;
+        if (nh > 0 && nh <= 32) {
+            h0 = ldg16(gout + ss);
+            if (nh > 16) h1 = ldg16(gout + ss + 16);
+        }
+    }
+    if (valid && L > 0) lane_copy(W + (o - ob), in + lp, L, sink);
+    if (n0 > nh) lane_copy(W + (m + nh - ob), W + (ss + nh - ob), n0 - nh, sink);
+    if (nh > 32) {
+        for (int32_t t = 0; t < nh; t += 64)
+            lane_copy64(W + (m + t - ob), gout + ss + t, nh - t < 64 ? nh - t : 64, gout + oend);
+    } else if (nh > 0) {
+        put16(W + (m - ob), h0, nh < 16 ? (uint32_t)nh : 16u, sink);
+        if (nh > 16) put16(W + (m + 16 - ob), h1, (uint32_t)(nh - 16), sink);
+    }
+    lockstep();  // literals and early match parts, read by other lanes next
+    // the rest: sources inside the batch
+    const int32_t a0 = lo & ~15;
+    lu8* span = W + (a0 - ob);
+    const int32_t ms2 = m + n0, m2 = M - n0, me = m + M;
+    const int32_t ss2 = ss + n0;
+    const int32_t need = me - off < ms2 ? me - off : ms2;  // source part before own output
+    uint64_t pending = ballot(valid && m2 > 0);
+    while (pending) {
+        const bool mine = (pending >> lane) & 1;
+        const int32_t mn = wave_excl_min(mine ? ms2 : INT32_MAX);
+        const int32_t mx = wave_excl_max(mine ? me : INT32_MIN);
+        const bool ready = mine && (need <= mn || ss2 >= mx);
+        const uint64_t rm = ballot(ready);
+        const uint32_t np = popc64(pending);
+        if ((rm == (pending & (0 - pending)) && np > 1) || (np >= 4 && 4 * popc64(rm) <= np)) {
+            const int32_t s0 = (int32_t)lane_val((uint32_t)ms2, ctz64(pending)) - a0;
+            resolve_chains(span, (lu16*)S.jump, lo - a0, hi - a0, s0, mine, ms2 - a0, m2, off, lane);
+            break;
+        }
+        if (ready) {
+            if (off != 0) lane_match(span + (ms2 - a0), (uint32_t)off, m2, sink);
+            else lane_zero(span + (ms2 - a0), m2, sink);
+        }
+        lockstep();
+        pending &= ~rm;
+    }
+    lockstep();
+    C.op = hi;
+    return nf;
+}
+
+// Loads 1 KiB of the block's input (window position r, block position pb) as
+// 4 dwords per lane; positions past the block read as 0.
+struct CkPf {
+    uint32_t w[4];
+};
+LZ4E_DEV CkPf ck_fetch(const ByteBuf& ib, int32_t sh, int32_t pb, uint32_t lane) {
+    CkPf f;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) f.w[j] = buf_ld32(ib, vaddr((uint32_t)(pb + sh + 4 * (int32_t)(lane + kWave * j))));
+    return f;
+}
+LZ4E_DEV void ck_put(CkLds& S, int32_t r, const CkPf& f, uint32_t lane) {
+    lu32* w = (lu32*)(S.in + r);
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j) w[lane + kWave * j] = f.w[j];
+}
+
+LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* gout, int32_t outSize,
+                        int32_t D, int32_t* ret_slot, uint32_t lane) {
+    const int32_t sh = (int32_t)(reinterpret_cast<uintptr_t>(in) & 3);
+    const ByteBuf ib = buf_make(in - sh, (uint32_t)((srcSize + sh + 3) & ~3));
+    const int32_t iend = srcSize, oend = outSize;
+    CkState C{-sh, 0, 0, 0};
+    bool wvalid = false;
+    int32_t ip = 0, n = 0, i = 0, X = 0;
+    bool stopped = false;
+    CkPf pf;
+    bool pfv = false;
+    for (uint32_t b = 0; b < 4; ++b) pf.w[b] = 0;
+    for (;;) {
+        bool exact = false;
+        if (i < n) {
+            if (C.op + kCkCap > C.ob + kCkOut) ck_slide(S, C, lane);
+            const uint32_t nb = ck_batch(S, C, i, n, iend, oend, D, gout, lane);
+            if (nb == 0) {
+                ip = C.wb + ck_pos(uni(((const lu32*)S.tok)[i]));
+                i++;
+                exact = true;
+            } else {
+                i += (int32_t)nb;
+                ip = C.wb + (i < n ? ck_pos(uni(((const lu32*)S.tok)[i])) : X);
+                if ((C.op & ~15) - C.fl >= kCkFlush) ck_flush(S, gout, C, C.op, false, lane);
+                if (i < n || !stopped) continue;
+                exact = true;  // the chain's stop: the exact path
+                n = 0;
+            }
+        } else if (ip > iend - 18) {
+            exact = true;  // past the fast region
+        } else {
+            // next chunk: the window must hold [ip, ip + 1 KiB) as its first half
+            const int32_t r = ip - C.wb;
+            if (wvalid && r >= kCkChunk && r < kCkIn) {
+                lu32* w = (lu32*)S.in;
+                uint32_t v[4];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) v[j] = w[kCkChunk / 4 + lane + kWave * j];
+                lockstep();
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) w[lane + kWave * j] = v[j];
+                C.wb += kCkChunk;
+                if (!pfv) pf = ck_fetch(ib, sh, C.wb + kCkChunk, lane);
+                ck_put(S, kCkChunk, pf, lane);
+            } else if (!wvalid || r < 0 || r >= kCkChunk) {
+                C.wb = ((ip + sh) & ~3) - sh;
+                ck_put(S, 0, ck_fetch(ib, sh, C.wb, lane), lane);
+                ck_put(S, kCkChunk, ck_fetch(ib, sh, C.wb + kCkChunk, lane), lane);
+                wvalid = true;
+            }
+            pfv = false;
+            lockstep();
+            const CkList Lst = ck_parse(S, ip - C.wb, iend - 18 - C.wb, lane);
+            // the next KiB, consumed when the window moves on
+            pf = ck_fetch(ib, sh, C.wb + kCkIn, lane);
+            pfv = true;
+            n = Lst.n;
+            i = 0;
+            X = Lst.x;
+            stopped = Lst.stp;
+            if (n > 0) continue;
+            if (!stopped) {
+                ip = C.wb + X;
+                continue;
+            }
+            ip = C.wb + X;
+            exact = true;
+        }
+        if (exact) {
+            // every byte before op into HBM, then one sequence there
+            ck_flush(S, gout, C, C.op, true, lane);
+            wave_fence();
+            bool done = false;
+            int32_t op = C.op;
+            const ParseResult pr = ck_exact(ib, sh, in, ip, op, iend, oend, D, done, gout, lane);
+            if (pr == kParseFail) {
+                if (lane == 0) *ret_slot = -ip - 1;
+                return;
+            }
+            if (done) {
+                if (lane == 0) *ret_slot = op;
+                return;
+            }
+            // the window restarts at the last 16-byte boundary
+            C.op = op;
+            C.ob = C.fl = op & ~15;
+            wave_fence();
+            if ((int32_t)lane < op - C.ob) ((lu8*)S.out)[lane] = *(const gu8*)(gout + C.ob + lane);
+            lockstep();
+            if (!(i < n && C.wb + ck_pos(uni(((const lu32*)S.tok)[i])) == ip)) {
+                n = 0;
+                i = 0;
+                stopped = false;
+            }
+        }
+    }
+}
+
+template <bool kStamps>
+__global__ __launch_bounds__(64) void decompress_chunk_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
+    const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
+    uint64_t* __restrict__ dbg, const int32_t* __restrict__ dict_len,
+    const uint32_t* __restrict__ order) {
+    __shared__ __attribute__((aligned(16))) CkLds S;
+    if (blockIdx.x >= nblocks) return;
+    const uint32_t b = order ? order[blockIdx.x] : blockIdx.x;
+    const uint32_t lane = lane_id();
+    const int32_t srcSize = src_len[b];
+    const int32_t outSize = dst_cap[b];
+    const uint8_t* in = src + src_off[b];
+    uint8_t* out = dst + dst_off[b];
+    (void)dbg;
+    if (special_case(in, srcSize, outSize, ret + b, lane)) return;
+    ck_decode(S, in, srcSize, out, outSize, dict_of(dict_len, b), ret + b, lane);
+}
+constexpr uint32_t kCkPerCu = (160u * 1024u) / sizeof(CkLds);
+
 // Blocks whose capacity is at least this take the pipelined decoder (small
 // blocks parse in a few batches; one wave each keeps more of them resident).
 constexpr uint32_t kPipeMinCap = 16384;
@@ -1963,8 +2584,28 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
     static const char* env = getenv("LZ4E_DECOMPRESS_MODE");
     uint32_t mode = a.mode;
     if (mode == kDecAuto && env)
-        mode = env[0] == 'w' ? kDecWave : (env[0] == 'p' ? kDecPipe : (env[0] == 's' ? kDecStream : kDecAuto));
+        mode = env[0] == 'w' ? kDecWave
+                             : (env[0] == 'p' ? kDecPipe
+                                              : (env[0] == 's' ? kDecStream : (env[0] == 'c' ? kDecChunk : kDecAuto)));
     if (mode == kDecAuto) mode = (a.max_cap == 0 || a.max_cap >= kPipeMinCap) ? kDecPipe : kDecWave;
+    if (mode == kDecChunk) {
+        const int om = launch_order_mode(false);
+        uint32_t* order = nullptr;
+        if ((om == kOrderAlways || (om == kOrderAuto && a.nblocks > 256 * kCkPerCu)) &&
+            hipMallocAsync((void**)&order, sizeof(uint32_t) * a.nblocks, stream) == hipSuccess) {
+            hipLaunchKernelGGL((order_kernel<DecodeWeight>), dim3(1), dim3(kOrderThreads), 0, stream,
+                               DecodeWeight{a.src_len, a.dst_cap}, a.nblocks, order);
+        } else {
+            (void)hipGetLastError();
+            order = nullptr;
+        }
+        hipLaunchKernelGGL((decompress_chunk_kernel<kStamps>), dim3(a.nblocks), dim3(kWave), 0, stream,
+                           a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
+                           dbg, a.dict_len, (const uint32_t*)order);
+        const hipError_t err = hipGetLastError();
+        if (order) (void)hipFreeAsync(order, stream);
+        return err;
+    }
     if (mode == kDecStream) {
         const int om = launch_order_mode(false);
         uint32_t* order = nullptr;

@@ -48,7 +48,7 @@ struct DecompressBatch {
     const int32_t* dict_len = nullptr;
 };
 
-enum : uint32_t { kDecAuto = 0, kDecWave = 1, kDecPipe = 2, kDecStream = 3 };
+enum : uint32_t { kDecAuto = 0, kDecWave = 1, kDecPipe = 2, kDecStream = 3, kDecChunk = 4 };
 
 // Launch order policy (lz4e_order.h): 0 block order, 1 heavy first when the
 // batch is large enough (default), 2 heavy first always.  From

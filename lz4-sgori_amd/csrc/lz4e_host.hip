@@ -22,6 +22,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -437,32 +438,59 @@ template <class Req>
 struct Coalescer {
     static constexpr int kMaxInflight = 4;    // concurrent batches (= HW queues of the process)
     static constexpr size_t kMaxBatch = 1024;
+    // A leader takes queued requests until their input reaches this (its own
+    // request always goes): one caller's huge request does not make a
+    // hundred small ones wait for its staging.
+    static constexpr uint64_t kMaxBatchBytes = 64ull << 20;
     std::mutex mu;
     std::condition_variable cv;
     std::vector<Req*> pending;
     int inflight = 0;
 
-    template <class Run>
-    void submit(Req* r, Run run) {
+    // run(batch, n) fills every request's result; fail(req, why) marks one
+    // failed.  Nothing in the leader's bookkeeping allocates, and run() is
+    // fenced: an exception there (std::bad_alloc in the batch's staging)
+    // fails that batch's requests -- every caller returns -- and the
+    // coalescer stays usable.
+    template <class Run, class Fail>
+    void submit(Req* r, Run run, Fail fail) {
         std::unique_lock<std::mutex> lk(mu);
-        pending.push_back(r);
+        try {
+            pending.push_back(r);
+        } catch (...) {
+            lk.unlock();
+            fail(r, "lz4e: out of host memory queueing the call");
+            return;
+        }
         while (!r->done) {
             if (!r->taken && inflight < kMaxInflight) {
-                std::vector<Req*> batch;
-                batch.push_back(r);
-                for (Req* q : pending)
-                    if (q != r && batch.size() < kMaxBatch) batch.push_back(q);
-                for (Req* q : batch) q->taken = true;
-                std::vector<Req*> rest;
-                for (Req* q : pending)
-                    if (!q->taken) rest.push_back(q);
-                pending.swap(rest);
+                Req* batch[kMaxBatch];
+                size_t n = 0;
+                uint64_t bytes = 0;
+                batch[n++] = r;
+                r->taken = true;
+                bytes += r->bytes();
+                for (Req* q : pending) {
+                    if (q->taken || n == kMaxBatch) continue;
+                    if (bytes + q->bytes() > kMaxBatchBytes) continue;
+                    bytes += q->bytes();
+                    q->taken = true;
+                    batch[n++] = q;
+                }
+                pending.erase(std::remove_if(pending.begin(), pending.end(), [](Req* q) { return q->taken; }),
+                              pending.end());
                 inflight++;
                 lk.unlock();
-                run(batch);
+                try {
+                    run(batch, n);
+                } catch (const std::exception& e) {
+                    for (size_t i = 0; i < n; ++i) fail(batch[i], std::string("lz4e: ") + e.what());
+                } catch (...) {
+                    for (size_t i = 0; i < n; ++i) fail(batch[i], "lz4e: exception in a coalesced batch");
+                }
                 lk.lock();
                 inflight--;
-                for (Req* q : batch) q->done = true;
+                for (size_t i = 0; i < n; ++i) batch[i]->done = true;
                 cv.notify_all();
             } else {
                 cv.wait(lk);
@@ -471,10 +499,24 @@ struct Coalescer {
     }
 };
 
+// decode_staging (defined with the C entry points below).
+uint64_t decode_staging_bytes(int csize, int cap);
+
+// Fault injection for the CPU test of the coalescer's unwinding
+// (lz4e_debug_coalescer_fault): the next k batch runs throw.
+std::atomic<int> g_coalescer_faults{0};
+void maybe_inject_fault() {
+    int k = g_coalescer_faults.load();
+    while (k > 0 && !g_coalescer_faults.compare_exchange_weak(k, k - 1)) {
+    }
+    if (k > 0) throw std::runtime_error("injected fault (lz4e_debug_coalescer_fault)");
+}
+
 struct CompressCall {
     lz4e_sg_request q;
     bool taken = false, done = false;
     std::string err;
+    uint64_t bytes() const { return q.srcIter->bi_size; }
 };
 
 struct DecompressCall {
@@ -483,15 +525,24 @@ struct DecompressCall {
     int csize, cap, ret = -1;
     bool taken = false, done = false;
     std::string err;
+    uint64_t bytes() const { return (uint64_t)std::max(csize, 0) + decode_staging_bytes(csize, cap); }
 };
 
+// One coalescer per device: a batch runs on its leader's current device, so
+// only requests from threads bound to the same device share it.
+constexpr int kMaxDevices = 64;
+int current_device() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) dev = 0;
+    return dev;
+}
 Coalescer<CompressCall>& compress_calls() {
-    static Coalescer<CompressCall> c;
-    return c;
+    static Coalescer<CompressCall> c[kMaxDevices];
+    return c[current_device()];
 }
 Coalescer<DecompressCall>& decompress_calls() {
-    static Coalescer<DecompressCall> c;
-    return c;
+    static Coalescer<DecompressCall> c[kMaxDevices];
+    return c[current_device()];
 }
 
 }  // namespace
@@ -508,16 +559,32 @@ int LZ4E_compress_default(const struct bio_vec* src, struct bio_vec* dst, struct
     if (srcIter->bi_size > LZ4E_MAX_INPUT_SIZE) return 0;
     CompressCall call;
     call.q = lz4e_sg_request{src, dst, srcIter, dstIter, 0};
-    compress_calls().submit(&call, [](std::vector<CompressCall*>& batch) {
-        std::vector<lz4e_sg_request> reqs;
-        reqs.reserve(batch.size());
-        for (CompressCall* c : batch) reqs.push_back(c->q);
-        const int r = compress_sg_batch_impl(reqs.data(), (int)reqs.size(), nullptr, nullptr);
-        for (size_t i = 0; i < batch.size(); ++i) {
-            batch[i]->q.ret = r < 0 ? 0 : reqs[i].ret;
-            batch[i]->err = g_err;
-        }
-    });
+    compress_calls().submit(
+        &call,
+        [](CompressCall** batch, size_t n) {
+            maybe_inject_fault();
+            std::vector<lz4e_sg_request> reqs(n);
+            for (size_t i = 0; i < n; ++i) reqs[i] = batch[i]->q;
+            int r = compress_sg_batch_impl(reqs.data(), (int)n, nullptr, nullptr);
+            if (r < 0 && n > 1) {
+                // the batch as a whole failed (staging, launch): each call
+                // alone, so that one caller's failure is not everyone's
+                for (size_t i = 0; i < n; ++i) {
+                    const int ri = compress_sg_batch_impl(&reqs[i], 1, nullptr, nullptr);
+                    batch[i]->q.ret = ri < 0 ? 0 : reqs[i].ret;
+                    batch[i]->err = g_err;
+                }
+                return;
+            }
+            for (size_t i = 0; i < n; ++i) {
+                batch[i]->q.ret = r < 0 ? 0 : reqs[i].ret;
+                batch[i]->err = g_err;
+            }
+        },
+        [](CompressCall* c, const std::string& why) {
+            c->q.ret = 0;
+            c->err = why;
+        });
     g_err = call.err;
     return call.q.ret;
 }
@@ -548,9 +615,13 @@ uint64_t decode_staging(int csize, int cap) {
     return std::min<uint64_t>((uint64_t)cap, most);
 }
 
+void lz4e_debug_coalescer_fault(int k) { g_coalescer_faults.store(k < 0 ? 0 : k); }
+
 }  // extern "C"
 
 namespace {
+
+uint64_t decode_staging_bytes(int csize, int cap) { return decode_staging(csize, cap); }
 
 // lz4e_decompress_batch, optionally with dictionaries: block i's output is
 // staged right after the last <= 64 KiB of its dictionary (the decoders read
@@ -640,26 +711,45 @@ int lz4e_decompress_batch(const char* const* src, const int* csize, char* const*
 
 int LZ4E_decompress_safe(const char* source, char* dest, int compressedSize, int maxDecompressedSize) {
     DecompressCall call{source, dest, compressedSize, maxDecompressedSize};
-    decompress_calls().submit(&call, [](std::vector<DecompressCall*>& batch) {
-        const size_t n = batch.size();
-        std::vector<const char*> src(n);
-        std::vector<char*> dst(n);
-        std::vector<int> cs(n), cap(n), ret(n, -1);
-        for (size_t i = 0; i < n; ++i) {
-            src[i] = batch[i]->src;
-            dst[i] = batch[i]->dst;
-            cs[i] = batch[i]->csize;
-            cap[i] = batch[i]->cap;
-        }
-        const int r = decompress_batch_impl(src.data(), cs.data(), dst.data(), cap.data(), ret.data(),
-                                            (int)n, nullptr, nullptr);
-        for (size_t i = 0; i < n; ++i) {
-            // a failed call: the block's own value if it has one (the
-            // watchdog's LZ4E_DECODE_ABORTED), else -1
-            batch[i]->ret = r < 0 ? (ret[i] < 0 ? ret[i] : -1) : ret[i];
-            batch[i]->err = g_err;
-        }
-    });
+    decompress_calls().submit(
+        &call,
+        [](DecompressCall** batch, size_t n) {
+            maybe_inject_fault();
+            std::vector<const char*> src(n);
+            std::vector<char*> dst(n);
+            std::vector<int> cs(n), cap(n), ret(n, -1);
+            for (size_t i = 0; i < n; ++i) {
+                src[i] = batch[i]->src;
+                dst[i] = batch[i]->dst;
+                cs[i] = batch[i]->csize;
+                cap[i] = batch[i]->cap;
+            }
+            const int r = decompress_batch_impl(src.data(), cs.data(), dst.data(), cap.data(), ret.data(),
+                                                (int)n, nullptr, nullptr);
+            if (r < 0 && n > 1) {
+                // the batch failed as a whole (staging, launch, a watchdog
+                // on some block): each call alone, so that only the caller
+                // whose block failed sees the failure
+                for (size_t i = 0; i < n; ++i) {
+                    int ri = -1;
+                    const int g = decompress_batch_impl(&src[i], &cs[i], &dst[i], &cap[i], &ri, 1, nullptr,
+                                                        nullptr);
+                    batch[i]->ret = g < 0 ? (ri < 0 ? ri : -1) : ri;
+                    batch[i]->err = g_err;
+                }
+                return;
+            }
+            for (size_t i = 0; i < n; ++i) {
+                // a failed call: the block's own value if it has one (the
+                // watchdog's LZ4E_DECODE_ABORTED), else -1
+                batch[i]->ret = r < 0 ? (ret[i] < 0 ? ret[i] : -1) : ret[i];
+                batch[i]->err = g_err;
+            }
+        },
+        [](DecompressCall* c, const std::string& why) {
+            c->ret = -1;
+            c->err = why;
+        });
     g_err = call.err;
     return call.ret;
 }

@@ -159,8 +159,11 @@ LZ4E_DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront
 // (LDS) or is ordered (global stores to one address) for every lane before
 // the wave's next one.  Marks the places that rely on it -- a whole-wave put
 // followed by a read-back, a lane's store overwriting bytes another lane
-// stored just before -- and emits no code.
-LZ4E_DEV void lockstep() {}
+// stored just before.  It emits no instruction, but it is a compiler memory
+// barrier: no access moves across it, whatever the access types (the
+// emulator's lockstep is a barrier of the emulated wave, so both builds
+// enforce the same order at the same places).
+LZ4E_DEV void lockstep() { asm volatile("" ::: "memory"); }
 // Workgroup barrier.
 LZ4E_DEV void block_sync() { __syncthreads(); }
 // Every global store of this wave has completed (before a flag says so).

@@ -123,3 +123,50 @@ def test_chunk_write_batch_no_gpu(amd):
     assert reqs[0].status == -lz4e_amd.EIO and reqs[0].comp_size == 0
     with pytest.raises(amd.GpuUnavailable):
         amd.chunk_write_batch([src])
+
+
+def test_coalescer_unwinds_a_throwing_batch(amd):
+    """The single-call coalescer (csrc/lz4e_host.hip, Coalescer::submit): when
+    a batch's run throws (here an injected fault, lz4e_debug_coalescer_fault;
+    in the field std::bad_alloc from its staging), every caller of that batch
+    returns -- a failure with the reason in lz4e_last_error -- and the next
+    calls are served, on a GPU box and off it."""
+    import threading
+
+    L = amd.lib()
+    L.lz4e_debug_coalescer_fault.argtypes = [ctypes.c_int]
+    L.lz4e_debug_coalescer_fault.restype = None
+    L.lz4e_last_error.restype = ctypes.c_char_p
+    L.lz4e_debug_coalescer_fault(1 << 20)
+    results = []
+
+    def caller(k):
+        for _ in range(4):
+            buf = ctypes.create_string_buffer(64)
+            r = L.LZ4E_decompress_safe(b"\x10a" * (1 + k % 3), buf, 2, 64)
+            results.append((r, L.lz4e_last_error().decode()))
+            data = b"abc" * 40
+            src = make_sg(data, [len(data)])
+            dst = make_sg(b"", [4096], capacity=256)
+            wrk = (ctypes.c_uint8 * lz4e_amd.LZ4E_MEM_COMPRESS)()
+            rc = L.LZ4E_compress_default(src.bvecs, dst.bvecs, ctypes.byref(src.it), ctypes.byref(dst.it), wrk)
+            results.append((rc - 1 if rc == 0 else rc, L.lz4e_last_error().decode()))
+
+    try:
+        ts = [threading.Thread(target=caller, args=(k,)) for k in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=60)
+        assert not any(t.is_alive() for t in ts), "a caller of a throwing batch never returned"
+    finally:
+        L.lz4e_debug_coalescer_fault(0)
+    assert len(results) == 64
+    assert all(r < 0 and "injected fault" in e for r, e in results), results[:4]
+    # the coalescer still serves calls
+    buf = ctypes.create_string_buffer(64)
+    r = L.LZ4E_decompress_safe(b"\x10a", buf, 2, 64)
+    if amd.gpu_available():
+        assert r == 1 and buf.raw[:1] == b"a"
+    else:
+        assert r < 0 and "injected" not in L.lz4e_last_error().decode()

@@ -126,13 +126,13 @@ def test_emulated_kernel_dictionary_sanitized(emu_exe, tmp_path, kind, n, dsize)
 # dictionary or a write past the capacity is caught
 # ---------------------------------------------------------------------------
 
-def _emu_decode(exe, tmp_path, frame, cap, dic=b""):
+def _emu_decode(exe, tmp_path, frame, cap, dic=b"", flag="-d"):
     f, o, d = tmp_path / "f.bin", tmp_path / "o.bin", tmp_path / "d.bin"
     f.write_bytes(frame)
     d.write_bytes(dic)
     if o.exists():
         o.unlink()
-    out = subprocess.run([exe, "-d", str(f), str(cap), str(o), str(d)], capture_output=True, text=True,
+    out = subprocess.run([exe, flag, str(f), str(cap), str(o), str(d)], capture_output=True, text=True,
                          timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "ERROR: AddressSanitizer" not in out.stderr and "runtime error" not in out.stderr
@@ -143,8 +143,9 @@ def _emu_decode(exe, tmp_path, frame, cap, dic=b""):
 DEC_CASES = [(k, m) for k in ("text", "records", "runs", "small_alpha") for m in range(5)]
 
 
+@pytest.mark.parametrize("flag", ["-d", "-c"], ids=["wave", "chunk"])
 @pytest.mark.parametrize("kind,mode", DEC_CASES, ids=[f"{k}-{m}" for k, m in DEC_CASES])
-def test_emulated_decoder_sanitized(emu_exe, tmp_path, kind, mode):
+def test_emulated_decoder_sanitized(emu_exe, tmp_path, kind, mode, flag):
     """Valid frames (mode 0), truncations (1), bit flips (2), short capacity
     (3) and a dictionary (4; with a shortened dictionary on odd seeds): the
     decoder's values, error codes and bytes equal the oracle's."""
@@ -167,7 +168,7 @@ def test_emulated_decoder_sanitized(emu_exe, tmp_path, kind, mode):
         elif mode == 4 and rep % 2:
             dic = dic[int(rng.integers(1, len(dic) - 8)):]
         want = oracle_ref.decompress_dict(f, cap, dic)
-        got = _emu_decode(emu_exe, tmp_path, f, cap, dic)
+        got = _emu_decode(emu_exe, tmp_path, f, cap, dic, flag)
         assert got[0] == want[0], (rep, got[0], want[0])
         if want[0] >= 0:
             assert got[1] == want[1], rep
@@ -251,10 +252,12 @@ def _emu_decode_pipe(exe, tmp_path, frame, cap, dic=b"", flag="-p"):
 PIPE_CASES = [(k, m) for k in ("text", "records", "ints", "runs") for m in range(5)] + [("random", 0)]
 
 
-@pytest.mark.parametrize("flag", ["-p", "-s"], ids=["pipe", "stream"])
+@pytest.mark.parametrize("flag", ["-p", "-s", "-c"], ids=["pipe", "stream", "chunk"])
 @pytest.mark.parametrize("kind,mode", PIPE_CASES, ids=[f"{k}-{m}" for k, m in PIPE_CASES])
 def test_emulated_pipe_decoder_sanitized(emu_exe, tmp_path, kind, mode, flag):
-    """The 4-wave pipelined decoder (-p) and the 2-wave streaming decoder (-s)
+    """The 4-wave pipelined decoder (-p), the 2-wave streaming decoder (-s)
+    and the one-wave chunked decoder (-c: speculative token walks, LDS output
+    window, HBM far sources)
     on 16-64 KiB blocks: valid frames (mode 0), truncations (1), bit flips
     (2), short capacity (3) and a dictionary (4): values, error codes and
     bytes equal the oracle's (/root/reference/lz4e/lz4e_decompress.c:62-460

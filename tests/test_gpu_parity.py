@@ -72,7 +72,7 @@ def _gpu_compress(amd, blocks, ttypes, caps=None):
     return r, frames, ax
 
 
-DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_STREAM = 0, 1, 2, 3
+DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_STREAM, DEC_CHUNK = 0, 1, 2, 3, 4
 
 
 def _gpu_decompress(amd, frames, caps, csizes=None, max_cap=None, mode=DEC_AUTO):
@@ -276,8 +276,9 @@ def test_decompress_batch_vs_oracle(gpu, kind):
         assert outs[i] == eo == expect[i]
 
 
+@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_CHUNK, DEC_PIPE, DEC_WAVE], ids=["auto", "chunk", "pipe", "wave"])
 @pytest.mark.parametrize("mode", ["truncate", "flip", "garbage", "small_cap", "csize"])
-def test_decompress_error_codes(gpu, mode):
+def test_decompress_error_codes(gpu, mode, dec):
     rng = np.random.default_rng(1234 + len(mode))
     data = _corpus("mixed", 1 << 20, 77)
     frames, caps, csizes = [], [], []
@@ -302,7 +303,7 @@ def test_decompress_error_codes(gpu, mode):
         frames.append(bytes(f))
         caps.append(cap)
         csizes.append(cs)
-    r, outs = _gpu_decompress(gpu, frames, caps, csizes)
+    r, outs = _gpu_decompress(gpu, frames, caps, csizes, mode=dec)
     for i in range(len(frames)):
         er, eo = oracle_ref.decompress(frames[i], caps[i], csize=csizes[i])
         assert r[i] == er, (i, mode, caps[i], csizes[i])
@@ -341,7 +342,7 @@ def test_full_size_roundtrip(gpu, cls, bs, kind):
         assert frames[i] == oracle_ref.compress(blocks[i], cls)[1]
 
 
-@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_STREAM], ids=["wave", "pipe", "stream"])
+@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_STREAM, DEC_CHUNK], ids=["wave", "pipe", "stream", "chunk"])
 def test_decompress_huge_runs(gpu, mode):
     """Blocks whose sequences are hundreds of MiB long: a 256 MiB run of one
     byte (a single match whose length extension is ~1 MiB of 0xFF) and a
@@ -360,7 +361,7 @@ def test_decompress_huge_runs(gpu, mode):
         assert outs[i] == b, i
 
 
-@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_STREAM], ids=["wave", "pipe", "stream"])
+@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_STREAM, DEC_CHUNK], ids=["wave", "pipe", "stream", "chunk"])
 @pytest.mark.parametrize("cap_extra", [0, 100000])
 def test_decompress_periodic_matches(gpu, cap_extra, mode):
     """Self-overlapping matches of every period 1..40 and lengths around
@@ -737,10 +738,11 @@ def test_decompress_pipelined_vs_wave_decoder(gpu, kind):
     r_wg, o_wg = _gpu_decompress(gpu, frames, caps, mode=DEC_PIPE)
     r_wv, o_wv = _gpu_decompress(gpu, frames, caps, mode=DEC_WAVE)
     r_st, o_st = _gpu_decompress(gpu, frames, caps, mode=DEC_STREAM)
+    r_ck, o_ck = _gpu_decompress(gpu, frames, caps, mode=DEC_CHUNK)
     for i, (er, eb) in enumerate(want):
-        assert r_wg[i] == er == r_wv[i] == r_st[i], (i, r_wg[i], er, r_wv[i], r_st[i])
+        assert r_wg[i] == er == r_wv[i] == r_st[i] == r_ck[i], (i, r_wg[i], er, r_wv[i], r_st[i], r_ck[i])
         if er >= 0:
-            assert o_wg[i] == eb == o_wv[i] == o_st[i], i
+            assert o_wg[i] == eb == o_wv[i] == o_st[i] == o_ck[i], i
 
 
 # ---------------------------------------------------------------------------
