@@ -410,12 +410,26 @@ def block_floor(b: "Batch", top: int = 8, reps: int = 5) -> dict:
     if rc != 0:
         raise SystemExit("bench: stamped compress failed: " + lz4e_amd.last_error())
     cyc = dbg.view(b.nblk, 8)[:, :6].sum(1).cpu().numpy()
+    one = torch.zeros(8, dtype=torch.int64, device=b.dev)
     worst = []
     for i in np.argsort(cyc)[::-1][:top]:
         i = int(i)
         sl = slice(i, i + 1)
-        best_c, best_d = 1e9, 1e9
+        # the block alone, stamped: its cycles with the chip to itself (a
+        # clock-free count: the same on every box)
+        one.zero_()
+        L.lz4e_debug_compress_stamped(b.d_src.data_ptr(), b.d_off[sl].data_ptr(), b.d_len[sl].data_ptr(),
+                                      b.d_tt[sl].data_ptr(), b.d_dst.data_ptr(), b.d_doff[sl].data_ptr(),
+                                      b.d_cap[sl].data_ptr(), b.d_ret[sl].data_ptr(), 1, b.bs,
+                                      b.stream.cuda_stream, one.data_ptr())
+        torch.cuda.synchronize(b.dev)
+        alone = int(one[:6].sum().item())
+        tcs, tds = [], []
         for _ in range(reps):
+            # a full-batch compress right before each timed pair: the lone
+            # wave runs at the clock the chip holds under this workload, not
+            # at an idle or boost clock of whatever ran before
+            b.compress()
             e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
             e0.record(b.stream)
             lz4e_amd.compress_batch_dev(b.d_src, b.d_off[sl], b.d_len[sl], b.d_tt[sl], b.d_dst,
@@ -427,14 +441,24 @@ def block_floor(b: "Batch", top: int = 8, reps: int = 5) -> dict:
                                           max_cap=b.bs)
             e2.record(b.stream)
             torch.cuda.synchronize(b.dev)
-            best_c, best_d = min(best_c, e0.elapsed_time(e1)), min(best_d, e1.elapsed_time(e2))
-        worst.append((best_c + best_d, best_c, best_d, i, int(cyc[i])))
+            tcs.append(e0.elapsed_time(e1))
+            tds.append(e1.elapsed_time(e2))
+        tc, td = float(np.median(tcs)), float(np.median(tds))
+        worst.append((tc + td, tc, td, i, int(cyc[i]), alone))
+    # restore the batch's frames (the single-block launches rewrote their own)
+    b.compress()
+    torch.cuda.synchronize(b.dev)
     worst.sort(reverse=True)
-    t, tc, td, i, c = worst[0]
+    t, tc, td, i, c, alone = worst[0]
+    clock = [a / (x[1] * 1e6) for x in worst if (a := x[5]) > 0 and x[1] > 0]
     return {"floor_ms": round(t, 4), "compress_ms": round(tc, 4), "decompress_ms": round(td, 4),
-            "block": i, "stamped_cycles_in_full_launch": c,
+            "block": i, "stamped_cycles_in_full_launch": c, "stamped_cycles_alone": alone,
+            "clock_ghz_est": round(float(np.median(clock)), 3) if clock else None,
+            "compress_ms_at_2_4ghz": round(alone / 2.4e6, 4),
             "method": f"the {top} blocks with the most stamped compress cycles, each compressed and "
-                      f"decoded alone (best of {reps}); the slowest sum is the floor"}
+                      f"decoded alone right after a full-batch compress (median of {reps}); the slowest "
+                      f"sum is the floor.  clock_ghz_est = the blocks' stamped cycles alone / their "
+                      f"compress time alone (launch overhead included, so a lower bound)"}
 
 
 def decompress_only(b: "Batch", steps: int, rank: int, world: int, dist, dev, traffic_json: str,

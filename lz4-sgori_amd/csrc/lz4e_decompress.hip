@@ -1999,6 +1999,10 @@ constexpr int32_t kCkOut = LZ4E_CK_OUT;       // output window
 constexpr int32_t kCkKeep = LZ4E_CK_KEEP;     // history kept when the window moves
 constexpr int32_t kCkCap = 1024;              // output bytes per fast batch
 constexpr int32_t kCkFlush = 2048;            // flush lag
+#ifndef LZ4E_CK_AHEAD
+#define LZ4E_CK_AHEAD 1
+#endif
+constexpr bool kCkAhead = LZ4E_CK_AHEAD;      // fields / far loads one batch ahead
 static_assert(kCkKeep >= kCkFlush + 32 && kCkOut >= kCkKeep + 2 * kCkCap && kCkOut % 16 == 0,
               "chunked decoder window sizes");
 
@@ -2310,11 +2314,17 @@ LZ4E_DEV void ck_flush(CkLds& S, uint8_t* gout, CkState& C, int32_t to, bool tai
     C.fl = tail ? to : (t16 > C.fl ? t16 : C.fl);
 }
 
-// Moves the output window forward (keeps the last kCkKeep bytes).
-LZ4E_DEV void ck_slide(CkLds& S, CkState& C, uint32_t lane) {
-    int32_t nob = (C.op - kCkKeep) & ~15;
-    nob = nob < C.fl ? nob : (C.fl & ~15);
-    if (nob <= C.ob) return;
+// The output window base for a batch that starts at op: unchanged while
+// the batch fits, else moved to keep the last kCkKeep bytes -- never past
+// the flushed prefix (everything before ob must be in HBM).
+LZ4E_DEV int32_t ck_ob_for(const CkState& C, int32_t op) {
+    if (op + kCkCap <= C.ob + kCkOut) return C.ob;
+    const int32_t a = (op - kCkKeep) & ~15, f = C.fl & ~15;
+    const int32_t nob = a < f ? a : f;
+    return nob > C.ob ? nob : C.ob;
+}
+// Moves the output window forward to nob (> C.ob).
+LZ4E_DEV void ck_slide(CkLds& S, CkState& C, int32_t nob, uint32_t lane) {
     lu8* W = (lu8*)S.out;
     const int32_t d = nob - C.ob, end = (C.op + 15) & ~15;
     // forward in 1 KiB steps: step s writes [1024 s, +1024), reads d bytes
@@ -2331,13 +2341,67 @@ LZ4E_DEV void ck_slide(CkLds& S, CkState& C, uint32_t lane) {
     C.ob = nob;
 }
 
-// One fast batch from list entry i (of n); returns the sequences decoded
-// (0: entry i takes the exact path).
-LZ4E_DEV uint32_t ck_batch(CkLds& S, CkState& C, int32_t i, int32_t n, int32_t iend, int32_t oend,
-                           int32_t D, uint8_t* gout, uint32_t lane) {
+// Whole-wave copies of one long piece (a sequence's literal run or match
+// part longer than kCkLong), 4 bytes per lane per step.  Source and
+// destination do not overlap (the input window, bytes before the batch, or
+// HBM bytes before the window).
+constexpr int32_t kCkLong = 32;
+LZ4E_DEV void ck_wave_copy(lu8* dst, const lu8* src, int32_t n, uint32_t lane) {
+    for (int32_t t0 = 0; t0 < n; t0 += 4 * (int32_t)kWave) {
+        const int32_t t = t0 + 4 * (int32_t)lane;
+        if (t + 4 <= n) st4(dst + t, ld4(src + t));
+        else
+            for (int32_t q = t; q < n; ++q) dst[q] = src[q];
+    }
+}
+LZ4E_DEV void ck_wave_fetch(lu8* dst, const uint8_t* src, int32_t n, uint32_t lane) {
+    for (int32_t t0 = 0; t0 < n; t0 += 4 * (int32_t)kWave) {
+        const int32_t t = t0 + 4 * (int32_t)lane;
+        if (t + 4 <= n) st4(dst + t, *(const gu32w*)(src + t));
+        else
+            for (int32_t q = t; q < n; ++q) dst[q] = *(const gu8*)(src + q);
+    }
+}
+// dst[t] = dst[t - off] for t < n in LZ order (any overlap; offset 0 writes
+// zeros): steps of at most D bytes read D bytes back, D a multiple of off
+// that doubles while 2 D <= t, so every step reads bytes written before it.
+LZ4E_DEV void ck_wave_match(lu8* dst, int32_t off, int32_t n, uint32_t lane) {
+    if (off == 0) {
+        for (int32_t t0 = 0; t0 < n; t0 += 4 * (int32_t)kWave) {
+            const int32_t t = t0 + 4 * (int32_t)lane;
+            if (t + 4 <= n) st4(dst + t, 0u);
+            else
+                for (int32_t q = t; q < n; ++q) dst[q] = 0;
+        }
+        return;
+    }
+    int32_t D = off;
+    for (int32_t t0 = 0; t0 < n;) {
+        int32_t c = n - t0 < 4 * (int32_t)kWave ? n - t0 : 4 * (int32_t)kWave;
+        c = c < D ? c : D;
+        const int32_t t = 4 * (int32_t)lane;
+        if (t + 4 <= c) st4(dst + t0 + t, ld4(dst + t0 + t - D));
+        else
+            for (int32_t q = t; q < c; ++q) dst[t0 + q] = dst[t0 + q - D];
+        lockstep();  // the next step reads these bytes
+        t0 += c;
+        while (2 * D <= t0) D *= 2;
+    }
+}
+
+// A fast batch: list entries [i, i + nf), sequence k in lane k, copied
+// under the output window base ob.  Its fields -- and the HBM part of its
+// early match sources -- are computed / loaded one batch ahead (ck_fields
+// for batch j + 1 runs before batch j's copies), so the HBM latency of far
+// sources hides under the previous batch's rounds.
+struct CkBatch {
+    int32_t i = -1, nf = 0, hi = 0, ob = 0;  // (wave-uniform)
+    int32_t o = 0, L = 0, M = 0, lp = 0, off = 0, n0 = 0, nh = 0;
+    uint4 h0 = {0, 0, 0, 0}, h1 = {0, 0, 0, 0};
+};
+LZ4E_DEV void ck_fields(CkLds& S, int32_t wb, int32_t i, int32_t n, int32_t op, int32_t ob, int32_t iend,
+                        int32_t oend, int32_t D, const uint8_t* gout, uint32_t lane, CkBatch& B) {
     const lu8* in = (const lu8*)S.in;
-    lu8* W = (lu8*)S.out;
-    lu8* sink = (lu8*)S.sink + 4 * lane;
     const int32_t idx = i + (int32_t)lane;
     const bool have = idx < n;
     const uint32_t e = have ? ((const lu32*)S.tok)[idx] : 0u;
@@ -2347,23 +2411,30 @@ LZ4E_DEV uint32_t ck_batch(CkLds& S, CkState& C, int32_t i, int32_t n, int32_t i
     const int32_t nx = lp + L + 2 + ck_ext(M - 4);
     const int32_t size = have ? L + M : 0;
     const int32_t incl = (int32_t)wave_incl_add((uint32_t)size);
-    const int32_t op = C.op;
     const int32_t o = op + incl - size, m = o + L;
     const bool ext = L >= 15 || M >= 19;
     // every check of the reference on this sequence passes (header comment)
     bool fast;
     if (ext)
-        fast = C.wb + nx <= iend - 17 && o + size <= oend - 32 && m - off + D >= 0;
+        fast = wb + nx <= iend - 17 && o + size <= oend - 32 && m - off + D >= 0;
     else
-        fast = C.wb + p <= iend - 18 && o <= oend - 32 &&
+        fast = wb + p <= iend - 18 && o <= oend - 32 &&
                (m >= off ? (off >= 8 || m + M <= oend - 5) : (m - off + D >= 0 && m + M <= oend - 5));
     const bool ok = have && fast && incl <= kCkCap;
     const uint64_t okm = ballot(ok);
     const uint32_t nf = (~okm) ? ctz64(~okm) : kWave;
-    if (nf == 0) return 0;
+    B.i = i;
+    B.nf = (int32_t)nf;
+    B.ob = ob;
+    if (nf == 0) return;
     const bool valid = lane < nf;
-    const int32_t lo = op, hi = op + (int32_t)lane_val((uint32_t)incl, nf - 1);
-    const int32_t ob = C.ob;
+    const int32_t lo = op;
+    B.hi = op + (int32_t)lane_val((uint32_t)incl, nf - 1);
+    B.o = o;
+    B.L = L;
+    B.M = M;
+    B.lp = lp;
+    B.off = off;
     // the part of the match whose source lies before the batch: final, from
     // the window, or from HBM before ob (flushed: ob <= fl)
     const int32_t ss = m - off;
@@ -2372,19 +2443,52 @@ LZ4E_DEV uint32_t ck_batch(CkLds& S, CkState& C, int32_t i, int32_t n, int32_t i
     if (valid && off != 0 && ss < lo) {
         n0 = M < lo - ss ? M : lo - ss;
         nh = ss < ob ? (n0 < ob - ss ? n0 : ob - ss) : 0;
-        if (nh > 0 && nh <= 32) {
+        if (nh > 0 && nh <= kCkLong) {
             h0 = ldg16(gout + ss);
             if (nh > 16) h1 = ldg16(gout + ss + 16);
         }
     }
-    if (valid && L > 0) lane_copy(W + (o - ob), in + lp, L, sink);
-    if (n0 > nh) lane_copy(W + (m + nh - ob), W + (ss + nh - ob), n0 - nh, sink);
-    if (nh > 32) {
-        for (int32_t t = 0; t < nh; t += 64)
-            lane_copy64(W + (m + t - ob), gout + ss + t, nh - t < 64 ? nh - t : 64, gout + oend);
-    } else if (nh > 0) {
+    B.n0 = n0;
+    B.nh = nh;
+    B.h0 = h0;
+    B.h1 = h1;
+}
+
+// The copies of batch B into the output window (C.ob == B.ob).
+LZ4E_DEV void ck_copy(CkLds& S, const CkBatch& B, int32_t oend, uint8_t* gout, uint32_t lane) {
+    const lu8* in = (const lu8*)S.in;
+    lu8* W = (lu8*)S.out;
+    lu8* sink = (lu8*)S.sink + 4 * lane;
+    const bool valid = (int32_t)lane < B.nf;
+    const int32_t ob = B.ob, lo = lane_val((uint32_t)B.o, 0), hi = B.hi;
+    const int32_t o = B.o, L = B.L, M = B.M, lp = B.lp, off = B.off, n0 = B.n0, nh = B.nh;
+    const int32_t m = o + L, ss = m - off;
+    const uint4 h0 = B.h0, h1 = B.h1;
+    // short pieces per lane, long ones (fio's 256-byte runs, long literals)
+    // by the whole wave, one piece after the other
+    const int32_t nw = n0 - nh;
+    const bool longL = valid && L > kCkLong, longW = nw > kCkLong, longH = nh > kCkLong;
+    if (valid && L > 0 && !longL) lane_copy(W + (o - ob), in + lp, L, sink);
+    if (nw > 0 && !longW) lane_copy(W + (m + nh - ob), W + (ss + nh - ob), nw, sink);
+    if (nh > 0 && !longH) {
         put16(W + (m - ob), h0, nh < 16 ? (uint32_t)nh : 16u, sink);
         if (nh > 16) put16(W + (m + 16 - ob), h1, (uint32_t)(nh - 16), sink);
+    }
+    for (uint64_t lm = ballot(longL); lm; lm &= lm - 1) {
+        const uint32_t k = ctz64(lm);
+        ck_wave_copy(W + ((int32_t)lane_val((uint32_t)o, k) - ob), in + lane_val((uint32_t)lp, k),
+                     (int32_t)lane_val((uint32_t)L, k), lane);
+    }
+    for (uint64_t lm = ballot(longW); lm; lm &= lm - 1) {
+        const uint32_t k = ctz64(lm);
+        const int32_t km = (int32_t)lane_val((uint32_t)m, k), kss = (int32_t)lane_val((uint32_t)ss, k);
+        const int32_t knh = (int32_t)lane_val((uint32_t)nh, k);
+        ck_wave_copy(W + (km + knh - ob), W + (kss + knh - ob), (int32_t)lane_val((uint32_t)nw, k), lane);
+    }
+    for (uint64_t lm = ballot(longH); lm; lm &= lm - 1) {
+        const uint32_t k = ctz64(lm);
+        const int32_t km = (int32_t)lane_val((uint32_t)m, k), kss = (int32_t)lane_val((uint32_t)ss, k);
+        ck_wave_fetch(W + (km - ob), gout + kss, (int32_t)lane_val((uint32_t)nh, k), lane);
     }
     lockstep();  // literals and early match parts, read by other lanes next
     // the rest: sources inside the batch
@@ -2406,16 +2510,20 @@ LZ4E_DEV uint32_t ck_batch(CkLds& S, CkState& C, int32_t i, int32_t n, int32_t i
             resolve_chains(span, (lu16*)S.jump, lo - a0, hi - a0, s0, mine, ms2 - a0, m2, off, lane);
             break;
         }
-        if (ready) {
+        const bool lng = m2 > 2 * kCkLong;
+        if (ready && !lng) {
             if (off != 0) lane_match(span + (ms2 - a0), (uint32_t)off, m2, sink);
             else lane_zero(span + (ms2 - a0), m2, sink);
         }
         lockstep();
+        for (uint64_t lm = ballot(ready && lng); lm; lm &= lm - 1) {
+            const uint32_t k = ctz64(lm);
+            ck_wave_match(span + ((int32_t)lane_val((uint32_t)ms2, k) - a0), (int32_t)lane_val((uint32_t)off, k),
+                          (int32_t)lane_val((uint32_t)m2, k), lane);
+        }
         pending &= ~rm;
     }
     lockstep();
-    C.op = hi;
-    return nf;
 }
 
 // Loads 1 KiB of the block's input (window position r, block position pb) as
@@ -2447,17 +2555,26 @@ LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* g
     CkPf pf;
     bool pfv = false;
     for (uint32_t b = 0; b < 4; ++b) pf.w[b] = 0;
+    CkBatch Bn;  // the next batch's fields, computed ahead (Bn.i < 0: none)
     for (;;) {
         bool exact = false;
         if (i < n) {
-            if (C.op + kCkCap > C.ob + kCkOut) ck_slide(S, C, lane);
-            const uint32_t nb = ck_batch(S, C, i, n, iend, oend, D, gout, lane);
-            if (nb == 0) {
+            CkBatch Bt;
+            if (Bn.i == i) Bt = Bn;
+            else ck_fields(S, C.wb, i, n, C.op, ck_ob_for(C, C.op), iend, oend, D, gout, lane, Bt);
+            Bn.i = -1;
+            if (Bt.nf == 0) {
                 ip = C.wb + ck_pos(uni(((const lu32*)S.tok)[i]));
                 i++;
                 exact = true;
             } else {
-                i += (int32_t)nb;
+                if (Bt.ob != C.ob) ck_slide(S, C, Bt.ob, lane);
+                const int32_t i2 = i + Bt.nf;
+                if (kCkAhead && i2 < n)
+                    ck_fields(S, C.wb, i2, n, Bt.hi, ck_ob_for(C, Bt.hi), iend, oend, D, gout, lane, Bn);
+                ck_copy(S, Bt, oend, gout, lane);
+                C.op = Bt.hi;
+                i = i2;
                 ip = C.wb + (i < n ? ck_pos(uni(((const lu32*)S.tok)[i])) : X);
                 if ((C.op & ~15) - C.fl >= kCkFlush) ck_flush(S, gout, C, C.op, false, lane);
                 if (i < n || !stopped) continue;
