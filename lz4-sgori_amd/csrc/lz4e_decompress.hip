@@ -1515,429 +1515,6 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
 }
 
 // ============================================================================
-// Streaming decoder: one block per 2-wave workgroup
-// ============================================================================
-//
-// Wave 0 parses exactly as in the pipelined decoder and publishes each batch
-// (records, output range, and for a fast batch the 512 input bytes of its
-// parse window) in a ring of record slots.  Wave 1 writes the output in
-// order, 256 bytes per step, lane l owning the dword at step offset 4l:
-//
-//  * owners: each sequence starting in the step marks its dword (LDS), a DPP
-//    max-scan gives every dword the last sequence started at or before it;
-//    a dword holds at most one sequence start (every fast sequence has a
-//    match of 4+ bytes), so two owners and four ds_bpermute gathers of the
-//    packed fields serve its four bytes;
-//  * sources: a literal byte comes from the slot's input window, a match
-//    byte from out[x - off] -- in LDS (an R-byte history ring of the output),
-//    in HBM when further back (stored earlier by this same wave, so in order:
-//    one vector L1 per CU), or in the step itself (pointer jumping over the
-//    step's 256 bytes, a chain of depth d in log2 d rounds); offset 0 writes
-//    zeros (lz4e_decompress.c:313, 407-415);
-//  * one dword per lane into the ring and one into HBM (byte stores only at
-//    the batch's two ends, so exactly [lo, hi) is written).
-//
-// No cross-wave ordering beyond the record slots: one wave writes every
-// output byte in order, so a source is final once its step has run.  A
-// scalar-path batch (long runs, block ends) copies in HBM as before, then
-// reloads the ring's last R bytes from HBM.  LDS ~11 KiB per block.
-#ifndef LZ4E_STREAM_RING
-#define LZ4E_STREAM_RING 4096
-#endif
-#ifndef LZ4E_STREAM_RECS
-#define LZ4E_STREAM_RECS 3
-#endif
-constexpr int32_t kSRing = LZ4E_STREAM_RING;  // power of two, >= 512
-constexpr uint32_t kSRecs = LZ4E_STREAM_RECS;
-constexpr int32_t kSOut = 2047;  // output bytes per fast batch (11-bit packed fields)
-constexpr int32_t kSStep = 4 * kWave;
-static_assert((kSRing & (kSRing - 1)) == 0 && kSRing >= 2 * kSStep, "ring size");
-enum { kSN, kSKind, kSLo, kSHi, kSBase, kSWords = 8 };
-
-struct StreamLds {
-    uint32_t ring[(kRing + kRingPad) / 4];  // parser input ring
-    int32_t rec[kSRecs][5][kWave];          // ls, L, op, off, M per sequence
-    int32_t hdr[kSRecs][kSWords];
-    uint32_t inp[kSRecs][2 * kWave];        // a fast batch's input window A|B (512 B)
-    uint32_t hist[kSRing / 4];              // output history ring
-    uint32_t mark[kWave];                   // per-step owner marks
-    uint64_t vp[kWave];                     // per-step (pointer << 8 | byte) x 4, pointer jumping
-    int32_t pub[kSRecs], con[kSRecs];
-    int32_t nb_total, abort, beat, result;
-};
-
-// Inclusive prefix max over the 64 lanes (values >= 0) with DPP.
-LZ4E_DEV uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
-LZ4E_DEV uint32_t wave_incl_umax(uint32_t v) {
-    uint32_t x = v;
-    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
-    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
-    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
-    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
-    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
-    x = umax(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
-    return x;
-}
-
-// Cycle counters of the stamped build (u64 per block): parser parse, parser
-// waits for a slot, copier waits for records, copier fast batches, copier
-// scalar batches (+ ring refill), batches, steps, steps with a far (HBM)
-// source, pointer-jumping rounds, steps with in-step sources.
-enum { kSsParse, kSsPWait, kSsRec, kSsFast, kSsScalar, kSsBatches, kSsSteps, kSsFarSteps,
-       kSsRounds, kSsPendSteps, kSsSlots };
-struct StreamStamps {
-    uint64_t t = 0, a[kSsSlots] = {};
-    LZ4E_DEV void lap(bool on, int k) {
-        if (!on) return;
-        const uint64_t now = clock64();
-        a[k] += now - t;
-        t = now;
-    }
-    LZ4E_DEV void add(bool on, int k, uint64_t v) {
-        if (on) a[k] += v;
-    }
-};
-
-// The HBM store of a step's dword, deferred by one step: issued after the
-// next step's far loads, so that those do not wait for it (a wave's loads and
-// stores complete in order).  Exactly one store instruction per step, every
-// lane active -- a lane with no byte of the batch rewrites lane 0's dword
-// with lane 0's value -- so that the compiler's vmcnt waits for the far
-// loads stay exact (a branch around a store makes them vmcnt(0), i.e. a
-// wait for the store).  Bytes of the dword before the batch carry their
-// final values (read back from the ring); bytes after it are rewritten by
-// the next batch (a batch that ends within 3 bytes of the capacity takes
-// stream_edge instead).
-struct PendStore {
-    uint32_t v = 0;
-    int32_t a = 0;
-    LZ4E_DEV void flush(uint8_t* gout) const { *(gu32w*)(gout + a) = v; }
-};
-
-// A step's byte sources (see stream_fast): LDS byte addresses, pointers
-// into the step (0xFF: none), zero / far / own-byte masks, far positions and
-// the far bytes (loaded when the descriptor is built, one step ahead of use).
-struct StepDesc {
-    uint32_t ao[4], fl[4], PT, zm, fm, bm;
-};
-
-// The output of fast batch [lo, hi) (records in b, input window at ibase in
-// the slot), 256 bytes per step (see above).  Software-pipelined: step t+1's
-// descriptor (owners, fields, sources, far loads) is built while step t's
-// gathers are in flight.
-template <bool kStamps>
-LZ4E_DEV void stream_fast(StreamLds& S, uint32_t slot, const Batch& b, int32_t lo, int32_t hi,
-                          int32_t ibase, uint8_t* gout, uint32_t lane, StreamStamps& st) {
-    const bool valid = lane < b.n;
-    // packed fields of sequence k (lane k): output start, match start and
-    // literal source relative to the batch / its window; the offset
-    const uint32_t P1 = valid ? (uint32_t)(b.op - lo) | ((uint32_t)(b.op + b.L - lo) << 11) |
-                                    ((uint32_t)(b.ls - ibase) << 22)
-                              : 0u;
-    const uint32_t P2 = valid ? (uint32_t)b.off : 0u;
-    lu8* const sb = (lu8*)&S;
-    const uint32_t h0 = (uint32_t)((lu8*)S.hist - sb);
-    const uint32_t i0 = (uint32_t)((lu8*)S.inp[slot] - sb);
-    lu32* mark = (lu32*)S.mark;
-    int32_t carry = -1;  // owner of the byte before the step
-    auto describe = [&](int32_t Xs, StepDesc& d) {
-        const int32_t x0 = Xs + 4 * (int32_t)lane;
-        mark[lane] = 0;
-        wave_fence();
-        const int32_t rs = b.op - Xs;
-        if (valid && rs >= 0 && rs < kSStep) mark[rs >> 2] = ((lane + 1) << 2) | (uint32_t)(rs & 3);
-        wave_fence();
-        const uint32_t m = mark[lane];
-        const uint32_t Mx = wave_incl_umax(m);
-        const int32_t o2 = Mx ? (int32_t)(Mx >> 2) - 1 : carry;
-        carry = (int32_t)lane_val((uint32_t)o2, kWave - 1);
-        const int32_t o1 = m ? o2 - 1 : o2;
-        const uint32_t j = m ? (m & 3) : 0;  // bytes q >= j are o2's
-        const uint32_t c1 = (uint32_t)(o1 < 0 ? 0 : o1), c2 = (uint32_t)(o2 < 0 ? 0 : o2);
-        const uint32_t A1 = shfl(P1, c1), B1 = shfl(P2, c1), A2 = shfl(P1, c2), B2 = shfl(P2, c2);
-        const int32_t flo = Xs - kSRing + 4;  // sources below this (or < 0) are read from HBM
-        // every byte's source, branch-free: an LDS byte address (ring or
-        // input window), an HBM position (far), a step byte (pending) or zero
-        d.PT = 0;
-        d.zm = 0;
-        d.fm = 0;
-        d.bm = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            const int32_t x = x0 + (int32_t)q;
-            const bool sec = q >= j;
-            const uint32_t A = sec ? A2 : A1, off = sec ? B2 : B1;
-            const int32_t xr = x - lo;
-            const int32_t op_r = (int32_t)(A & 0x7FFu), ms_r = (int32_t)((A >> 11) & 0x7FFu);
-            const int32_t ls_r = (int32_t)(A >> 22);
-            const bool before = xr < 0, past = x >= hi;
-            const bool lit = !before && xr < ms_r;
-            const bool mt = !before && !past && !lit;
-            const int32_t src = x - (int32_t)off;
-            const bool cp = mt && off != 0;
-            const bool pend = cp && src >= Xs;
-            const bool ring = cp && src < Xs && src >= flo && src >= 0;
-            const bool far = cp && !pend && !ring;
-            const uint32_t hx = h0 + (uint32_t)(x & (kSRing - 1)), hs = h0 + (uint32_t)(src & (kSRing - 1));
-            const uint32_t il = i0 + (uint32_t)(ls_r + xr - op_r);
-            d.ao[q] = before ? hx : (lit ? il : (ring ? hs : h0));
-            d.PT |= (pend ? (uint32_t)(src - Xs) : 0xFFu) << (8 * q);
-            d.zm |= (past || (mt && off == 0) ? 1u : 0u) << q;
-            d.fm |= (far ? 1u : 0u) << q;
-            d.bm |= (!before && !past ? 1u : 0u) << q;
-            // far byte (always loaded: a fixed number of loads per step keeps
-            // the compiler's waits exact; a non-far lane reads byte lo)
-            d.fl[q] = *(const gu8*)(gout + (far ? src : lo));
-        }
-    };
-    // gathers, in-step pointer jumping, ring write; the step's HBM store
-    // (deferred, see PendStore) into `out`
-    auto step = [&](int32_t Xs, const StepDesc& cur, PendStore& out) {
-        const int32_t x0 = Xs + 4 * (int32_t)lane;
-        lockstep();  // the previous step's ring dwords, read by other lanes
-        uint32_t g[4];
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) g[q] = sb[cur.ao[q]];
-        if (kStamps) {
-            st.add(true, kSsSteps, 1);
-            st.add(true, kSsFarSteps, ballot(cur.fm != 0) != 0);
-            st.add(true, kSsPendSteps, ballot(cur.PT != 0xFFFFFFFFu) != 0);
-        }
-        uint32_t V = 0, PT = cur.PT;
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            const uint32_t v = ((cur.fm >> q) & 1) ? cur.fl[q] : (((cur.zm >> q) & 1) ? 0u : g[q]);
-            V |= (v & 0xFFu) << (8 * q);
-        }
-        // in-step sources: pointer jumping (the pointer of byte t names the
-        // step byte it copies; 0xFF = final)
-        if (ballot(PT != 0xFFFFFFFFu)) {
-            const lu16* vt = (const lu16*)S.vp;
-            for (;;) {
-                uint64_t w = 0;
-#pragma unroll
-                for (uint32_t q = 0; q < 4; ++q)
-                    w |= (uint64_t)((((PT >> (8 * q)) & 0xFFu) << 8) | ((V >> (8 * q)) & 0xFFu)) << (16 * q);
-                *(lu64*)&S.vp[lane] = w;
-                wave_fence();  // (u16 reads of u64 stores: no type-based reordering)
-                uint32_t e[4];
-#pragma unroll
-                for (uint32_t q = 0; q < 4; ++q) {
-                    const uint32_t p = (PT >> (8 * q)) & 0xFFu;
-                    e[q] = vt[p == 0xFFu ? 0u : p];  // (unconditional: all in flight together)
-                }
-                uint32_t PN = 0, VN = 0;
-#pragma unroll
-                for (uint32_t q = 0; q < 4; ++q) {
-                    const uint32_t p = (PT >> (8 * q)) & 0xFFu;
-                    const uint32_t tp = e[q] >> 8;
-                    PN |= (p == 0xFFu ? 0xFFu : tp) << (8 * q);
-                    VN |= ((p != 0xFFu && tp == 0xFFu) ? (e[q] & 0xFFu) : ((V >> (8 * q)) & 0xFFu)) << (8 * q);
-                }
-                PT = PN;
-                V = VN;
-                st.add(kStamps, kSsRounds, 1);
-                if (!ballot(PT != 0xFFFFFFFFu)) break;
-            }
-        }
-        lockstep();  // (every gather of the step before the ring write)
-        const bool mine = x0 < hi;
-        if (mine) *(lu32*)(sb + h0 + (uint32_t)(x0 & (kSRing - 1))) = V;
-        const uint32_t V0 = lane_val(V, 0);
-        out.v = mine ? V : V0;
-        out.a = mine ? x0 : Xs;
-    };
-    // (Building step t+1's descriptor before step t's gathers -- a software
-    // pipeline -- measured slower: 5.4k -> 6.1k cycles per text batch.)
-    PendStore ps;
-    for (int32_t Xs = lo & ~3; Xs < hi; Xs += kSStep) {
-        StepDesc cur;
-        describe(Xs, cur);
-        if (Xs != (lo & ~3)) ps.flush(gout);  // the previous step's dword (after the far loads)
-        step(Xs, cur, ps);
-    }
-    ps.flush(gout);
-}
-
-// A fast batch ending within 3 bytes of the block's capacity: its
-// sequences one at a time in HBM (lane 0, exact bytes), then the ring.
-LZ4E_DEV void stream_edge(const Batch& b, const uint8_t* in, int32_t srcSize, uint8_t* gout,
-                          int32_t outSize, uint32_t lane) {
-    for (uint32_t k = 0; k < b.n; ++k) {
-        Batch one;
-        const bool me = lane == 0;
-        one.ls = me ? (int32_t)lane_val((uint32_t)b.ls, k) : 0;
-        one.L = me ? (int32_t)lane_val((uint32_t)b.L, k) : 0;
-        one.op = me ? (int32_t)lane_val((uint32_t)b.op, k) : 0;
-        one.off = me ? (int32_t)lane_val((uint32_t)b.off, k) : 0;
-        one.M = me ? (int32_t)lane_val((uint32_t)b.M, k) : 0;
-        one.n = 1;
-        copy_scalar_hbm(one, in, srcSize, gout, outSize, lane);
-    }
-}
-
-// After an in-HBM batch [lo, hi): the history ring's bytes from HBM (the
-// copies were this wave's own stores: in order).
-LZ4E_DEV void stream_refill(StreamLds& S, int32_t lo, int32_t hi, const uint8_t* gout, uint32_t lane) {
-    int32_t g0 = (hi & ~3) - kSRing + 4;
-    g0 = (g0 > lo ? g0 : lo) & ~3;
-    lu8* hist = (lu8*)S.hist;
-    for (int32_t g = g0 + 4 * (int32_t)lane; g < hi; g += kSStep) {
-        uint32_t v = 0;
-        if (g + 4 <= hi) {
-            v = *(const gcu32*)(const void*)(gout + g);
-        } else {
-            for (int32_t q = 0; g + q < hi; ++q) v |= (uint32_t)gout[g + q] << (8 * q);
-        }
-        *(lu32*)(hist + (g & (kSRing - 1))) = v;
-    }
-    wave_fence();
-}
-
-// Streaming decoder kernel: LDS ~11 KiB and two waves per block, so a
-// whole 64 KiB-block batch of the Silesia size is resident at once.
-// (waves per SIMD: 7 = 14 two-wave blocks per CU, the LDS limit at ~11 KiB)
-#ifndef LZ4E_STREAM_WAVES_PER_EU
-#define LZ4E_STREAM_WAVES_PER_EU 7
-#endif
-template <bool kStamps>
-__global__ __launch_bounds__(2 * kWave, LZ4E_STREAM_WAVES_PER_EU) void decompress_stream_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
-    const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
-    const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
-    uint64_t* __restrict__ dbg, const int32_t* __restrict__ dict_len,
-    const uint32_t* __restrict__ order) {
-    __shared__ __attribute__((aligned(16))) StreamLds S;
-    if (blockIdx.x >= nblocks) return;
-    const uint32_t b = order ? order[blockIdx.x] : blockIdx.x;
-    const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
-    const int32_t srcSize = src_len[b];
-    const int32_t outSize = dst_cap[b];
-    const uint8_t* in = src + src_off[b];
-    uint8_t* gout = dst + dst_off[b];
-    if (special_case(in, srcSize, outSize, ret + b, tid)) return;
-    StreamStamps st;
-    if (kStamps) st.t = clock64();
-    if (tid < kSRecs) {
-        S.pub[tid] = -1;
-        S.con[tid] = (int32_t)tid - (int32_t)kSRecs;
-    }
-    if (tid == 0) {
-        S.nb_total = INT32_MAX;
-        S.abort = 0;
-        S.beat = 0;
-        S.result = kPipeAbort;
-    }
-    __syncthreads();
-
-    if (wave == 0) {
-        // ---------------- parser (as in decompress_pipe_kernel) ----------------
-        // (issue priority: the copier is this kernel's critical path; parser
-        // 1 / copier 3 measured 0.95 -> 0.90 ms on silesia64k against 3 / 0)
-        __builtin_amdgcn_s_setprio(1);
-        Parse P;
-        P.init(in, srcSize, outSize, (lu32*)S.ring, lane, dict_of(dict_len, b));
-        int32_t j = 0;
-        for (;;) {
-            Batch bt;
-            const int32_t lo = P.op;
-            const ParseResult pr = parse_batch<true>(P, bt, lane, kSOut);
-            st.lap(kStamps, kSsParse);
-            if (pr == kParseFail) {
-                if (lane == 0) S.result = -P.ip - 1;
-                break;
-            }
-            const uint32_t slot = (uint32_t)j % kSRecs;
-            if (!wait_for(S, [&] { return lds_acquire(&S.con[slot]) == j - (int32_t)kSRecs; },
-                          [&] { return lds_acquire(&S.beat) + lds_acquire(&S.con[slot]); })) {
-                lds_release(&S.abort, 1);
-                break;
-            }
-            st.lap(kStamps, kSsPWait);
-            S.rec[slot][0][lane] = bt.ls;
-            S.rec[slot][1][lane] = bt.L;
-            S.rec[slot][2][lane] = bt.op;
-            S.rec[slot][3][lane] = bt.off;
-            S.rec[slot][4][lane] = bt.M;
-            if (pr == kParsedFast) {
-                S.inp[slot][lane] = P.win.a;
-                S.inp[slot][kWave + lane] = P.win.b;
-            }
-            if (lane < kSWords) {
-                const int32_t h[kSWords] = {(int32_t)bt.n, pr == kParsedScalar ? kKindHbm : kKindFast,
-                                            lo, P.op, P.win.base, 0, 0, 0};
-                int32_t v = 0;
-#pragma unroll
-                for (uint32_t q = 0; q < kSWords; ++q) v = lane == q ? h[q] : v;
-                S.hdr[slot][lane] = v;
-            }
-            lds_release(&S.pub[slot], j);
-            j++;
-            if (P.done) {
-                if (lane == 0) S.result = P.op;
-                break;
-            }
-        }
-        lds_release(&S.nb_total, j);
-    } else {
-        // ---------------- copier ----------------
-        __builtin_amdgcn_s_setprio(3);
-        for (int32_t j = 0;; ++j) {
-            const uint32_t slot = (uint32_t)j % kSRecs;
-            const bool ok = wait_for(
-                S, [&] { return lds_acquire(&S.pub[slot]) == j || lds_acquire(&S.nb_total) <= j; },
-                [&] { return lds_acquire(&S.beat) + lds_acquire(&S.pub[slot]); });
-            st.lap(kStamps, kSsRec);
-            if (!ok) {
-                lds_release(&S.abort, 1);
-                break;
-            }
-            if (lds_acquire(&S.pub[slot]) != j) break;  // the parser ended before batch j
-            st.add(kStamps, kSsBatches, 1);
-            Batch bt;
-            bt.ls = S.rec[slot][0][lane];
-            bt.L = S.rec[slot][1][lane];
-            bt.op = S.rec[slot][2][lane];
-            bt.off = S.rec[slot][3][lane];
-            bt.M = S.rec[slot][4][lane];
-            int32_t hdr[kSWords];
-#pragma unroll
-            for (uint32_t q = 0; q < kSWords; ++q) hdr[q] = (int32_t)uni((uint32_t)S.hdr[slot][q]);
-            bt.n = (uint32_t)hdr[kSN];
-            if (hdr[kSKind] == kKindHbm) {
-                lds_release(&S.con[slot], j);
-                copy_scalar_hbm<4>(bt, in, srcSize, gout, outSize, lane, [&] {
-                    if (lane == 0)
-                        __hip_atomic_fetch_add(&S.beat, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                });
-                stream_refill(S, hdr[kSLo], hdr[kSHi], gout, lane);
-                st.lap(kStamps, kSsScalar);
-            } else if (hdr[kSHi] + 3 > outSize) {
-                lds_release(&S.con[slot], j);
-                stream_edge(bt, in, srcSize, gout, outSize, lane);
-                stream_refill(S, hdr[kSLo], hdr[kSHi], gout, lane);
-                st.lap(kStamps, kSsScalar);
-            } else {
-                stream_fast<kStamps>(S, slot, bt, hdr[kSLo], hdr[kSHi], hdr[kSBase], gout, lane, st);
-                lds_release(&S.con[slot], j);
-                st.lap(kStamps, kSsFast);
-            }
-        }
-    }
-    __syncthreads();
-    if (tid == 0) ret[b] = __hip_atomic_load(&S.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                               ? kPipeAbort
-                               : S.result;
-    if constexpr (kStamps) {
-        if (lane == 0 && dbg) {
-            uint64_t* d = dbg + kStSlots * (size_t)b;
-            for (int k = 0; k < kSsSlots; ++k)
-                if (st.a[k]) atomicAdd((unsigned long long*)(d + k), (unsigned long long)st.a[k]);
-        }
-    }
-}
-
-// ============================================================================
 // Chunked decoder: one wave per block, a token list per 1 KiB of input
 // ============================================================================
 //
@@ -1995,6 +1572,10 @@ constexpr int32_t kCkChunk = 1024;            // compressed bytes per chunk
 constexpr int32_t kCkSeg = 16;                // ... per lane
 constexpr int32_t kCkIn = 2 * kCkChunk;       // input window
 constexpr int32_t kCkSlots = 6;               // tokens per segment at most (3+ bytes each)
+#ifndef LZ4E_CK_WARM
+#define LZ4E_CK_WARM 16
+#endif
+constexpr int32_t kCkWarm = LZ4E_CK_WARM;     // warm-up bytes of a speculative walk
 constexpr int32_t kCkOut = LZ4E_CK_OUT;       // output window
 constexpr int32_t kCkKeep = LZ4E_CK_KEEP;     // history kept when the window moves
 constexpr int32_t kCkCap = 1024;              // output bytes per fast batch
@@ -2003,6 +1584,14 @@ constexpr int32_t kCkFlush = 2048;            // flush lag
 #define LZ4E_CK_AHEAD 1
 #endif
 constexpr bool kCkAhead = LZ4E_CK_AHEAD;      // fields / far loads one batch ahead
+#ifndef LZ4E_CK_PJ
+#define LZ4E_CK_PJ 1
+#endif
+constexpr bool kCkPJ = LZ4E_CK_PJ;            // pointer jumping when few matches are ready
+#ifndef LZ4E_CK_PJMIN
+#define LZ4E_CK_PJMIN 8
+#endif
+constexpr uint32_t kCkPJMin = LZ4E_CK_PJMIN;  // ... and at least this many pending
 static_assert(kCkKeep >= kCkFlush + 32 && kCkOut >= kCkKeep + 2 * kCkCap && kCkOut % 16 == 0,
               "chunked decoder window sizes");
 
@@ -2068,22 +1657,41 @@ struct CkWalk {
     int32_t x = 0;
     bool stp = false;
 };
+// A walk may start before ss (a warm-up: chains started at different
+// positions merge within a few tokens, so a walk that starts kCkWarm bytes
+// early has usually joined the true chain when it enters its segment); only
+// tokens inside the segment are recorded.
 LZ4E_DEV CkWalk ck_walk(const lu8* in, lu32* slot, int32_t p, int32_t ss, int32_t se, int32_t plim) {
     CkWalk w;
-    while (p < se) {  // at most kCkSlots tokens
+    while (p < se) {  // at most kCkSlots tokens recorded (+ the warm-up's)
         uint32_t e;
         int32_t nx;
         if (p > plim || !ck_token(in, p, e, nx)) {
             w.stp = true;
             break;
         }
-        w.vis |= 1u << (p - ss);
-        slot[w.cnt++] = e;
+        if (p >= ss) {
+            w.vis |= 1u << (p - ss);
+            slot[w.cnt++] = e;
+        }
         p = nx;
     }
     w.x = p;
     return w;
 }
+
+// Cycle / event counters of the chunked decoder's stamped build (per block,
+// u64 x kCkSt into dbg; lane 0 accumulates).
+enum { kCkParse, kCkPRounds, kCkChunks, kCkFields, kCkCopy, kCkBatches, kCkSeqs, kCkExact, kCkNExact,
+       kCkFlushSlide, kCkRounds, kCkNPJ, kCkTotal, kCkCopyPre, kCkSt = 16 };
+struct CkSt {
+    uint64_t t = 0, a[kCkSt] = {};
+    LZ4E_DEV void lap(int k) {
+        const uint64_t now = clock64();
+        a[k] += now - t;
+        t = now;
+    }
+};
 
 // The chunk's tokens from the true entry E (window position in [0, kCkChunk)):
 // the list in S.tok[0, n), the chain's exit x (first position past the
@@ -2092,20 +1700,31 @@ struct CkList {
     int32_t n = 0, x = 0;
     bool stp = false;
 };
-LZ4E_DEV CkList ck_parse(CkLds& S, int32_t E, int32_t plim, uint32_t lane) {
+template <bool kSt>
+LZ4E_DEV CkList ck_parse(CkLds& S, int32_t E, int32_t plim, uint32_t lane, CkSt& stp) {
     const int32_t ss = kCkSeg * (int32_t)lane, se = ss + kCkSeg;
     const uint32_t l0 = (uint32_t)E >> 4;
     const bool act = lane >= l0;
     const lu8* in = (const lu8*)S.in;
     lu32* slot = (lu32*)S.tok + kCkSlots * lane;
     int32_t T = lane == l0 ? E : ss;  // assumed first token of the true chain in the segment
-    int32_t st = T;                   // where this lane's walk started
+    // where this lane's walk starts: the entry itself (lane l0, or a lane
+    // whose warm-up would reach back to it), else kCkWarm bytes early
+    int32_t st = lane == l0 ? E : (ss - kCkWarm > E ? ss - kCkWarm : E);
     bool sf = false;                  // the true chain stopped before this segment
     CkWalk w;
     w.x = se;
-    if (act) w = ck_walk(in, slot, T, ss, se, plim);
+    if (act) w = ck_walk(in, slot, st, ss, se, plim);
     bool settled = false;
-    for (uint32_t it = 0; it < kWave + 2; ++it) {
+    // Parallel rounds settle dense chains (every lane holds tokens: the
+    // hand-over from the lane before is nearly always a position its own walk
+    // passed through) in one or two rounds.  Where the chain jumps over lanes
+    // (long literal runs) a round only carries the entry one lane further,
+    // so after kCkRounds rounds the hand-over goes lane by lane along the
+    // chain instead (one step per lane that holds a true token).
+    constexpr uint32_t kCkRounds = 3;
+    for (uint32_t it = 0; it < kCkRounds; ++it) {
+        if constexpr (kSt) stp.a[kCkPRounds]++;
         // hand-over from the lane before: its true chain's first position in this segment
         const int32_t pT = shfl_up(T, 1), px = shfl_up(w.x, 1);
         const int32_t pf = shfl_up((sf ? 1 : 0) | (w.stp ? 2 : 0), 1);
@@ -2138,11 +1757,40 @@ LZ4E_DEV CkList ck_parse(CkLds& S, int32_t E, int32_t plim, uint32_t lane) {
         }
     }
     CkList r;
-    if (!settled) {  // (cannot happen: each round settles the next lane) -- the exact path decides
-        r.n = 0;
-        r.x = E;
-        r.stp = true;
-        return r;
+    bool scanned = false;
+    if (!settled) {
+        scanned = true;
+        T = INT32_MAX;  // lanes the chain does not stop in: no tokens
+        sf = false;
+        int32_t Tu = E;
+        uint32_t l = l0;
+        r.stp = false;
+        while (l < kWave) {
+            if constexpr (kSt) stp.a[kCkPRounds]++;
+            const int32_t ssl = kCkSeg * (int32_t)l;
+            const int32_t stl = (int32_t)lane_val((uint32_t)st, l);
+            const uint32_t visl = lane_val(w.vis, l);
+            int32_t xl = (int32_t)lane_val((uint32_t)w.x, l);
+            uint32_t stpl = lane_val(w.stp ? 1u : 0u, l);
+            const bool consl = (Tu >= stl && ((visl >> (Tu - ssl)) & 1u)) || (stpl && xl == Tu);
+            if (!consl) {
+                if (lane == l) {
+                    st = Tu;
+                    w = ck_walk(in, slot, Tu, ss, se, plim);
+                }
+                xl = (int32_t)lane_val((uint32_t)w.x, l);
+                stpl = lane_val(w.stp ? 1u : 0u, l);
+            }
+            if (lane == l) T = Tu;
+            if (stpl) {
+                r.stp = true;
+                Tu = xl;
+                break;
+            }
+            Tu = xl;  // >= the next segment
+            l = (uint32_t)Tu >> 4;
+        }
+        r.x = Tu;
     }
     // this lane's true tokens: its slots from T on
     uint32_t j0 = 0, nt = 0;
@@ -2162,6 +1810,7 @@ LZ4E_DEV CkList ck_parse(CkLds& S, int32_t E, int32_t plim, uint32_t lane) {
         if (q < nt) list[base + q] = e[q];
     lockstep();
     r.n = (int32_t)lane_val(incl, kWave - 1);
+    if (scanned) return r;
     // the exit: what lane 63 hands over
     const int32_t T63 = (int32_t)lane_val((uint32_t)T, kWave - 1);
     const int32_t x63 = (int32_t)lane_val((uint32_t)w.x, kWave - 1);
@@ -2455,7 +2104,8 @@ LZ4E_DEV void ck_fields(CkLds& S, int32_t wb, int32_t i, int32_t n, int32_t op, 
 }
 
 // The copies of batch B into the output window (C.ob == B.ob).
-LZ4E_DEV void ck_copy(CkLds& S, const CkBatch& B, int32_t oend, uint8_t* gout, uint32_t lane) {
+template <bool kSt>
+LZ4E_DEV void ck_copy(CkLds& S, const CkBatch& B, int32_t oend, uint8_t* gout, uint32_t lane, CkSt& stp) {
     const lu8* in = (const lu8*)S.in;
     lu8* W = (lu8*)S.out;
     lu8* sink = (lu8*)S.sink + 4 * lane;
@@ -2491,6 +2141,7 @@ LZ4E_DEV void ck_copy(CkLds& S, const CkBatch& B, int32_t oend, uint8_t* gout, u
         ck_wave_fetch(W + (km - ob), gout + kss, (int32_t)lane_val((uint32_t)nh, k), lane);
     }
     lockstep();  // literals and early match parts, read by other lanes next
+    if constexpr (kSt) stp.lap(kCkCopyPre);
     // the rest: sources inside the batch
     const int32_t a0 = lo & ~15;
     lu8* span = W + (a0 - ob);
@@ -2499,13 +2150,17 @@ LZ4E_DEV void ck_copy(CkLds& S, const CkBatch& B, int32_t oend, uint8_t* gout, u
     const int32_t need = me - off < ms2 ? me - off : ms2;  // source part before own output
     uint64_t pending = ballot(valid && m2 > 0);
     while (pending) {
+        if constexpr (kSt) stp.a[kCkRounds]++;
         const bool mine = (pending >> lane) & 1;
         const int32_t mn = wave_excl_min(mine ? ms2 : INT32_MAX);
         const int32_t mx = wave_excl_max(mine ? me : INT32_MIN);
         const bool ready = mine && (need <= mn || ss2 >= mx);
         const uint64_t rm = ballot(ready);
         const uint32_t np = popc64(pending);
-        if ((rm == (pending & (0 - pending)) && np > 1) || (np >= 4 && 4 * popc64(rm) <= np)) {
+        // pointer jumping pays only for chains of many short matches (records,
+        // integer tables); long matches (fio's 256-byte runs) go in rounds
+        if (kCkPJ && np >= kCkPJMin && 4 * popc64(rm) <= np && !ballot(mine && m2 > 2 * kCkLong)) {
+            if constexpr (kSt) stp.a[kCkNPJ]++;
             const int32_t s0 = (int32_t)lane_val((uint32_t)ms2, ctz64(pending)) - a0;
             resolve_chains(span, (lu16*)S.jump, lo - a0, hi - a0, s0, mine, ms2 - a0, m2, off, lane);
             break;
@@ -2543,8 +2198,19 @@ LZ4E_DEV void ck_put(CkLds& S, int32_t r, const CkPf& f, uint32_t lane) {
     for (uint32_t j = 0; j < 4; ++j) w[lane + kWave * j] = f.w[j];
 }
 
+template <bool kSt>
 LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* gout, int32_t outSize,
-                        int32_t D, int32_t* ret_slot, uint32_t lane) {
+                        int32_t D, int32_t* ret_slot, uint32_t lane, uint64_t* dbg) {
+    CkSt st;
+    if constexpr (kSt) st.t = clock64();
+    const uint64_t t00 = kSt ? st.t : 0;
+    auto finish = [&]() {
+        if constexpr (kSt) {
+            st.a[kCkTotal] = clock64() - t00;
+            if (lane == 0 && dbg)
+                for (int k = 0; k < kCkSt; ++k) dbg[k] = st.a[k];
+        }
+    };
     const int32_t sh = (int32_t)(reinterpret_cast<uintptr_t>(in) & 3);
     const ByteBuf ib = buf_make(in - sh, (uint32_t)((srcSize + sh + 3) & ~3));
     const int32_t iend = srcSize, oend = outSize;
@@ -2559,20 +2225,29 @@ LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* g
     for (;;) {
         bool exact = false;
         if (i < n) {
+            if constexpr (kSt) st.lap(kCkFlushSlide);
             CkBatch Bt;
             if (Bn.i == i) Bt = Bn;
             else ck_fields(S, C.wb, i, n, C.op, ck_ob_for(C, C.op), iend, oend, D, gout, lane, Bt);
             Bn.i = -1;
+            if constexpr (kSt) st.lap(kCkFields);
             if (Bt.nf == 0) {
                 ip = C.wb + ck_pos(uni(((const lu32*)S.tok)[i]));
                 i++;
                 exact = true;
             } else {
                 if (Bt.ob != C.ob) ck_slide(S, C, Bt.ob, lane);
+                if constexpr (kSt) st.lap(kCkFlushSlide);
                 const int32_t i2 = i + Bt.nf;
                 if (kCkAhead && i2 < n)
                     ck_fields(S, C.wb, i2, n, Bt.hi, ck_ob_for(C, Bt.hi), iend, oend, D, gout, lane, Bn);
-                ck_copy(S, Bt, oend, gout, lane);
+                if constexpr (kSt) {
+                    st.lap(kCkFields);
+                    st.a[kCkBatches]++;
+                    st.a[kCkSeqs] += (uint64_t)Bt.nf;
+                }
+                ck_copy<kSt>(S, Bt, oend, gout, lane, st);
+                if constexpr (kSt) st.lap(kCkCopy);
                 C.op = Bt.hi;
                 i = i2;
                 ip = C.wb + (i < n ? ck_pos(uni(((const lu32*)S.tok)[i])) : X);
@@ -2605,7 +2280,8 @@ LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* g
             }
             pfv = false;
             lockstep();
-            const CkList Lst = ck_parse(S, ip - C.wb, iend - 18 - C.wb, lane);
+            if constexpr (kSt) st.lap(kCkFlushSlide);
+            const CkList Lst = ck_parse<kSt>(S, ip - C.wb, iend - 18 - C.wb, lane, st);
             // the next KiB, consumed when the window moves on
             pf = ck_fetch(ib, sh, C.wb + kCkIn, lane);
             pfv = true;
@@ -2613,6 +2289,10 @@ LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* g
             i = 0;
             X = Lst.x;
             stopped = Lst.stp;
+            if constexpr (kSt) {
+                st.lap(kCkParse);
+                st.a[kCkChunks]++;
+            }
             if (n > 0) continue;
             if (!stopped) {
                 ip = C.wb + X;
@@ -2622,18 +2302,25 @@ LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* g
             exact = true;
         }
         if (exact) {
+            if constexpr (kSt) st.lap(kCkFlushSlide);
             // every byte before op into HBM, then one sequence there
             ck_flush(S, gout, C, C.op, true, lane);
             wave_fence();
             bool done = false;
             int32_t op = C.op;
             const ParseResult pr = ck_exact(ib, sh, in, ip, op, iend, oend, D, done, gout, lane);
+            if constexpr (kSt) {
+                st.lap(kCkExact);
+                st.a[kCkNExact]++;
+            }
             if (pr == kParseFail) {
                 if (lane == 0) *ret_slot = -ip - 1;
+                finish();
                 return;
             }
             if (done) {
                 if (lane == 0) *ret_slot = op;
+                finish();
                 return;
             }
             // the window restarts at the last 16-byte boundary
@@ -2666,15 +2353,22 @@ __global__ __launch_bounds__(64) void decompress_chunk_kernel(
     const int32_t outSize = dst_cap[b];
     const uint8_t* in = src + src_off[b];
     uint8_t* out = dst + dst_off[b];
-    (void)dbg;
     if (special_case(in, srcSize, outSize, ret + b, lane)) return;
-    ck_decode(S, in, srcSize, out, outSize, dict_of(dict_len, b), ret + b, lane);
+    ck_decode<kStamps>(S, in, srcSize, out, outSize, dict_of(dict_len, b), ret + b, lane,
+                       kStamps && dbg ? dbg + kStSlots * (size_t)b : nullptr);
 }
 constexpr uint32_t kCkPerCu = (160u * 1024u) / sizeof(CkLds);
 
-// Blocks whose capacity is at least this take the pipelined decoder (small
-// blocks parse in a few batches; one wave each keeps more of them resident).
+// Blocks whose capacity lies in [kPipeMinCap, kPipeMaxCap) take the
+// pipelined decoder.  Small blocks parse in a few batches, and one wave each
+// keeps more of them resident.  Large blocks (256 KiB: ~560 batches each)
+// decode faster one wave per block as well: 20 resident blocks per CU
+// against 6 four-wave ones, so a 3 815-block batch runs in one round of
+// workgroups instead of 2.5 (text256k decompress-only 4.33 -> 3.04 ms,
+// profiles/r04/decmodes.txt); at 64 KiB the pipelined decoder's per-block
+// speed wins (silesia64k 0.85 vs 1.20 ms).
 constexpr uint32_t kPipeMinCap = 16384;
+constexpr uint32_t kPipeMaxCap = 131072;
 
 // Launch order of the pipelined decoder when the batch takes more than one
 // round of workgroups (lz4e_order.h): a block's decode time grows with its
@@ -2682,7 +2376,6 @@ constexpr uint32_t kPipeMinCap = 16384;
 // their capacity (stored / incompressible data: a few long literal runs) are
 // the lightest.
 constexpr uint32_t kOrderMin = 256 * (24 / kPipeWaves);  // one round of pipelined workgroups
-constexpr uint32_t kStreamOrderMin = 256 * 2 * LZ4E_STREAM_WAVES_PER_EU;  // one round of streaming ones
 struct DecodeWeight {
     const int32_t* src_len;
     const int32_t* dst_cap;
@@ -2701,10 +2394,9 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
     static const char* env = getenv("LZ4E_DECOMPRESS_MODE");
     uint32_t mode = a.mode;
     if (mode == kDecAuto && env)
-        mode = env[0] == 'w' ? kDecWave
-                             : (env[0] == 'p' ? kDecPipe
-                                              : (env[0] == 's' ? kDecStream : (env[0] == 'c' ? kDecChunk : kDecAuto)));
-    if (mode == kDecAuto) mode = (a.max_cap == 0 || a.max_cap >= kPipeMinCap) ? kDecPipe : kDecWave;
+        mode = env[0] == 'w' ? kDecWave : (env[0] == 'p' ? kDecPipe : (env[0] == 'c' ? kDecChunk : kDecAuto));
+    if (mode == kDecAuto)
+        mode = (a.max_cap == 0 || (a.max_cap >= kPipeMinCap && a.max_cap < kPipeMaxCap)) ? kDecPipe : kDecWave;
     if (mode == kDecChunk) {
         const int om = launch_order_mode(false);
         uint32_t* order = nullptr;
@@ -2719,24 +2411,6 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
         hipLaunchKernelGGL((decompress_chunk_kernel<kStamps>), dim3(a.nblocks), dim3(kWave), 0, stream,
                            a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
                            dbg, a.dict_len, (const uint32_t*)order);
-        const hipError_t err = hipGetLastError();
-        if (order) (void)hipFreeAsync(order, stream);
-        return err;
-    }
-    if (mode == kDecStream) {
-        const int om = launch_order_mode(false);
-        uint32_t* order = nullptr;
-        if ((om == kOrderAlways || (om == kOrderAuto && a.nblocks > kStreamOrderMin)) &&
-            hipMallocAsync((void**)&order, sizeof(uint32_t) * a.nblocks, stream) == hipSuccess) {
-            hipLaunchKernelGGL((order_kernel<DecodeWeight>), dim3(1), dim3(kOrderThreads), 0, stream,
-                               DecodeWeight{a.src_len, a.dst_cap}, a.nblocks, order);
-        } else {
-            (void)hipGetLastError();
-            order = nullptr;
-        }
-        hipLaunchKernelGGL((decompress_stream_kernel<kStamps>), dim3(a.nblocks), dim3(2 * kWave), 0,
-                           stream, a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.nblocks, dbg, a.dict_len, (const uint32_t*)order);
         const hipError_t err = hipGetLastError();
         if (order) (void)hipFreeAsync(order, stream);
         return err;

@@ -3,8 +3,6 @@
 //   emu_main -d FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (one-wave decoder)
 //   emu_main -p FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (pipelined decoder,
 //            4 waves: parser + 3 copiers)
-//   emu_main -s FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (streaming decoder,
-//            2 waves: parser + in-order copier)
 //   emu_main -c FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (chunked decoder,
 //            one wave)
 // compresses one block through the unmodified kernel source, prints the
@@ -61,8 +59,8 @@ static int decode_main(int argc, char** argv) {
     // the decoder reads the input window by aligned dwords (the GPU's word
     // granularity: the dword holding the last byte); the heap block covers it
     frame.reserve((frame.size() + 3) & ~(size_t)3);
-    // kDecPipe / kDecStream / kDecChunk / kDecWave
-    const uint32_t mode = argv[1][1] == 'p' ? 2u : (argv[1][1] == 's' ? 3u : (argv[1][1] == 'c' ? 4u : 1u));
+    // kDecPipe / kDecChunk / kDecWave
+    const uint32_t mode = argv[1][1] == 'p' ? 2u : (argv[1][1] == 'c' ? 4u : 1u);
     emu_decompress_batch_mode(frame.data(), &so, &csize, out.data(), &doff, &cap, &ret, 1, &D, mode);
     char err[256];
     const int good = emu_decode_results(&ret, 1, err, sizeof err);
@@ -78,7 +76,7 @@ static int decode_main(int argc, char** argv) {
 
 int main(int argc, char** argv) {
     if (argc > 3 && argv[1][0] == '-' &&
-        (argv[1][1] == 'd' || argv[1][1] == 'p' || argv[1][1] == 's' || argv[1][1] == 'c'))
+        (argv[1][1] == 'd' || argv[1][1] == 'p' || argv[1][1] == 'c'))
         return decode_main(argc, argv);
     if (argc < 3) {
         fprintf(stderr, "usage: emu_main BLOCK_FILE TABLE_CLASS [FRAME_OUT]\n");
