@@ -37,6 +37,7 @@
 // end of the frame: every match is followed by at least the last-literals
 // token and 5 literals.
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -359,10 +360,18 @@ LZ4E_DEV uint64_t lane_range(uint32_t a, uint32_t b) {
 //    so a search over the window is "first probe lane with a hit", every
 //    probe before it put; probes with larger steps go to the generic search.
 // The window's puts are written to the table once, when the walk leaves it.
+// The block's results: the frame size (0: output full) and the iterator
+// post-state words (final source position, last literal run).  Returned, not
+// stored here: the kernel stores them through pointers it reloads after the
+// parse, so that no output pointer occupies SGPRs across it.
+struct CResult {
+    int32_t ret = 0;
+    uint32_t a0 = 0, a1 = 0;
+};
 template <int TT, bool kStamps, class IMG>
-LZ4E_DEV void compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* out, uint32_t cap,
-                             int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg, uint32_t lane,
-                             uint32_t D = 0, bool progress_prio = true) {
+LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* out, uint32_t cap,
+                                uint64_t* dbg, uint32_t lane, uint32_t D = 0, bool progress_prio = true) {
+    CResult res;
     // Dictionary mode (D > 0): the image is [D dictionary bytes | the n-byte
     // block], the parse starts at D and the table was preloaded from the
     // dictionary; positions are image positions throughout.
@@ -1007,13 +1016,9 @@ last_literals: {
             op += 1;
         }
         out_copy_exact(out, op, img, anchor, R, lane);
-        if (lane == 0) {
-            *ret_slot = (int32_t)(op + R);
-            if (aux_slot) {
-                aux_slot[0] = ip - D;
-                aux_slot[1] = R;
-            }
-        }
+        res.ret = (int32_t)(op + R);
+        res.a0 = ip - D;
+        res.a1 = R;
         if (kStamps) {
             st.lap(kPhTail);
             if (lane == 0 && dbg) {
@@ -1022,16 +1027,10 @@ last_literals: {
                 dbg[7] = ((uint64_t)st.cnt[3] << 32) | st.cnt[2];
             }
         }
-        return;
+        return res;
     }
 fail:
-    if (lane == 0) {
-        *ret_slot = 0;
-        if (aux_slot) {
-            aux_slot[0] = 0;
-            aux_slot[1] = 0;
-        }
-    }
+    return res;  // 0, 0, 0
 }
 
 // Stage a block into LDS as a word image, the bytes of the last partial word
@@ -1064,16 +1063,37 @@ LZ4E_DEV void stage_block(uint32_t* dstw, const uint8_t* src, uint32_t n, uint32
 }
 
 template <bool kStamps, class IMG>
-LZ4E_DEV void dispatch_class(const IMG& img, uint32_t* smem, uint32_t n, int tt, gu8* out,
-                             uint32_t cap, int32_t* ret_slot, uint32_t* aux_slot, uint64_t* dbg,
-                             uint32_t lane, uint32_t D = 0, bool pp = true) {
-    if (tt == kByU32)
-        compress_block<kByU32, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, D, pp);
-    else if (tt == kByU16)
-        compress_block<kByU16, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, 0, pp);
-    else
-        compress_block<kByU64, kStamps>(img, smem, n, out, cap, ret_slot, aux_slot, dbg, lane, 0, pp);
+LZ4E_DEV CResult dispatch_class(const IMG& img, uint32_t* smem, uint32_t n, int tt, gu8* out,
+                                uint32_t cap, uint64_t* dbg, uint32_t lane, uint32_t D = 0,
+                                bool pp = true) {
+    if (tt == kByU32) return compress_block<kByU32, kStamps>(img, smem, n, out, cap, dbg, lane, D, pp);
+    if (tt == kByU16) return compress_block<kByU16, kStamps>(img, smem, n, out, cap, dbg, lane, 0, pp);
+    return compress_block<kByU64, kStamps>(img, smem, n, out, cap, dbg, lane, 0, pp);
 }
+
+// The kernel's explicit arguments as laid out in the kernarg segment
+// (natural alignment, in order).  After the parse the kernel reloads its
+// result pointers from there through a laundered pointer -- a fresh scalar
+// load -- instead of keeping them live in SGPRs across the whole parse
+// (which is at the SGPR limit: every pointer held there is one more spill
+// reloaded inside the window loops).
+struct CompressArgs {
+    const uint8_t* src;
+    const uint64_t* src_off;
+    const uint32_t* src_len;
+    const uint8_t* table_type;
+    uint8_t* dst;
+    const uint64_t* dst_off;
+    const uint32_t* dst_cap;
+    int32_t* ret;
+    uint32_t* aux;
+    uint32_t nblocks;
+    uint32_t max_len;
+    uint64_t* dbg;
+    const uint32_t* dict_len;
+    const uint32_t* order;
+};
+static_assert(offsetof(CompressArgs, ret) == 56 && offsetof(CompressArgs, order) == 96, "kernarg layout");
 
 template <bool kLdsInput, bool kStamps>
 __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict__ src,
@@ -1097,7 +1117,6 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
     const uint32_t cap = dst_cap[b];
     gu8* out = (gu8*)(dst + dst_off[b]);
     const uint8_t* in = src + src_off[b];
-    uint32_t* aux_slot = aux ? aux + 2 * (size_t)b : nullptr;
     uint64_t* dbg_slot = dbg ? dbg + 8 * (size_t)b : nullptr;
 
     // Dictionary mode: the dict_len[b] (<= 64 KiB) bytes before the block
@@ -1116,6 +1135,7 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
         return;
     }
 
+    CResult res;
     if (n >= kMinLength) {
         // memset of the state (lz4e_compress.c:548): 16 KiB of table.
         uint4* t4 = reinterpret_cast<uint4*>(smem);
@@ -1127,7 +1147,7 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
         stage_block(inw, in, n, lane);
         block_sync();
         const LdsImage img{inw, n == 0 ? 0 : (n - 1) >> 2};
-        dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane);
+        res = dispatch_class<kStamps>(img, smem, n, tt, out, cap, dbg_slot, lane);
     } else {
         block_sync();
         const uint8_t* base = in - D;
@@ -1154,7 +1174,28 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
                 if (blockIdx.x < nh) __builtin_amdgcn_s_setprio(3);
             }
         }
-        dispatch_class<kStamps>(img, smem, n, tt, out, cap, ret + b, aux_slot, dbg_slot, lane, D, pp);
+        res = dispatch_class<kStamps>(img, smem, n, tt, out, cap, dbg_slot, lane, D, pp);
+    }
+    // results, through pointers reloaded now (see CompressArgs)
+#ifndef LZ4E_EMU
+    const __attribute__((address_space(4))) CompressArgs* ka =
+        (const __attribute__((address_space(4))) CompressArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(ka));
+    int32_t* const retp = ka->ret;
+    uint32_t* const auxp = ka->aux;
+    const uint32_t* const ordp = ka->order;
+#else
+    int32_t* const retp = ret;
+    uint32_t* const auxp = aux;
+    const uint32_t* const ordp = order;
+#endif
+    const uint32_t b2 = ordp ? ordp[blockIdx.x] : blockIdx.x;
+    if (lane == 0) {
+        retp[b2] = res.ret;
+        if (auxp) {
+            auxp[2 * (size_t)b2] = res.a0;
+            auxp[2 * (size_t)b2 + 1] = res.a1;
+        }
     }
 }
 
