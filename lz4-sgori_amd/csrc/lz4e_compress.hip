@@ -377,7 +377,10 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
     // dictionary; positions are image positions throughout.
     const Table<TT> T{smem};
     const uint64_t bound = (uint64_t)n + n / 255 + 16;
-    const bool limited = cap < bound;  // lz4e_compress.c:553-560
+    // limited output (lz4e_compress.c:553-560): the output checks compare
+    // against capl, which is the capacity when limited and never reached
+    // otherwise (one SGPR instead of a flag and the capacity)
+    const uint32_t capl = cap < bound ? cap : 0xFFFFFFFFu;
     uint32_t op = 0, anchor = D, ip = D;
     [[maybe_unused]] uint32_t trn = 0;
     Stamps st;
@@ -400,7 +403,7 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
         auto emit_match = [&](uint32_t tok, uint32_t tokhi, uint32_t off, uint32_t mc) -> bool {
             const uint32_t op_off = op;
             op += 2;
-            if (limited && (uint64_t)op + 6 + (mc >> 8) > cap) return false;
+            if ((uint64_t)op + 6 + (mc >> 8) > capl) return false;
             const uint32_t tokb = tokhi | (mc < 15 ? mc : 15);
             const uint32_t e1 = mc - 15;
             const uint32_t e1w = (mc >= 15 && e1 < 255) ? e1 : 0;
@@ -434,8 +437,8 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
         // q = floor(4 (e - D) / n) moves only at the quarter marks, so the
         // window loop compares e against the next mark (a division per
         // window costs ~25 instructions and two VALU -> SALU hops).
-        uint32_t prio_q = (n > 16384 && progress_prio) ? 4 : 5;
-        uint32_t prio_next = prio_q == 5 ? ~0u : D;  // e - D at which q changes next
+        // (q only grows: each crossing of a mark is a new quarter)
+        uint32_t prio_next = (n > 16384 && progress_prio) ? D : ~0u;  // e at which q changes next
         // Put pattern the clash fixpoint starts from for the lanes ahead of a
         // chain: every lane, or (periodic data: ints, records) the previous
         // window's final puts, whichever predicted the last window better.
@@ -455,10 +458,7 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
             if (e >= prio_next) {
                 const uint32_t q = (uint32_t)(((uint64_t)(e - D) * 4) / n);
                 prio_next = q >= 4 ? ~0u : D + (uint32_t)(((uint64_t)(q + 1) * n + 3) / 4);
-                if (q != prio_q) {
-                    prio_q = q;
-                    wave_prio_for(q);
-                }
+                wave_prio_for(q);
             }
             consume(pf);
             const uint32_t B = rmode ? e - 2 : e;
@@ -579,7 +579,7 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
 
             // ================= walk =========================================
             for (;;) {
-                if (rmode && !limited) {
+                if (rmode && capl == 0xFFFFFFFFu) {
                     // ---- fast chain: follow fc from the current rmode lane ----
                     // With clash lanes ahead, a candidate is "the latest put of
                     // its group before it", and the puts are the chain's own:
@@ -720,7 +720,7 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
                         }
                     }
                 }
-                if (kStamps && rmode && !limited) { st.cnt[3]++; st.lap(kPhLit); }
+                if (kStamps && rmode && capl == 0xFFFFFFFFu) { st.cnt[3]++; st.lap(kPhLit); }
                 if (rmode) {
                     // ---- fill table at e-2, test e (lz4e_compress.c:461-493) ----
                     const uint32_t k = e - B;
@@ -842,7 +842,7 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
                 // literals [anchor, ipm) (lz4e_compress.c:352-382)
                 const uint32_t L = ipm - anchor;
                 const uint32_t tok = op++;
-                if (limited && (uint64_t)op + L + 8 + L / 255 > cap) goto fail;
+                if ((uint64_t)op + L + 8 + L / 255 > capl) goto fail;
                 uint32_t tokhi;
                 if (L >= 15) {
                     tokhi = 0xF0;
@@ -979,7 +979,7 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
                 LZ4E_TR(2, ipm, ((uint64_t)cand << 32) | t);
                 const uint32_t L = ipm - anchor;
                 const uint32_t tok = op++;
-                if (limited && (uint64_t)op + L + 8 + L / 255 > cap) goto fail;
+                if ((uint64_t)op + L + 8 + L / 255 > capl) goto fail;
                 uint32_t tokhi;
                 if (L >= 15) {
                     tokhi = 0xF0;
@@ -1006,7 +1006,7 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
 last_literals: {
         // lz4e_compress.c:500-530
         const uint32_t R = D + n - anchor;
-        if (limited && (uint64_t)op + R + 1 + (R + 240) / 255 > cap) goto fail;
+        if ((uint64_t)op + R + 1 + (R + 240) / 255 > capl) goto fail;
         if (R >= 15) {
             if (lane == 0) out[op] = 0xF0;
             op += 1;
