@@ -80,24 +80,26 @@ struct Table {
 
 // A block in HBM, read with unaligned vector loads (gfx950 global loads need
 // no alignment).  n >= kMinLength whenever the parse runs.
+// Every access is a buffer load through one resource (4 SGPRs for the whole
+// image: no separate base pointer or length held across the parse, which is
+// at the SGPR limit), its offset forced into a VGPR (a uniform offset would
+// otherwise become s_buffer_load, which ignores the low two address bits).
 struct HbmImage {
-    gcu8* p;
-    uint32_t n;
-    ByteBuf buf;  // the same bytes as a buffer resource (window loads)
-    LZ4E_DEV uint32_t rd8(uint32_t q) const { return p[q]; }
+    ByteBuf buf;  // the block (and its dictionary) as a buffer resource
+    LZ4E_DEV uint32_t rd8(uint32_t q) const { return buf_ld8(buf, vaddr(q)); }
     // Window loads: dword at q, 0 when any of its bytes lies outside the
     // block (callers never use such a dword: every compared byte is in one
     // fully inside); buffer loads take the constant part of the offset in
     // the instruction and merge into dwordx4.
     LZ4E_DEV uint32_t wld(uint32_t q) const { return buf_ld32(buf, q); }
-    LZ4E_DEV uint32_t ld32(uint32_t q) const { return *(gcu32*)(p + vaddr(q)); }
-    LZ4E_DEV uint64_t ld64(uint32_t q) const { return *(gcu64*)(p + vaddr(q)); }
-    // Lanes past the block (or before it, X < 4) read a clamped, meaningless
-    // dword; every consumer masks those bytes.
-    LZ4E_DEV uint32_t stripe(uint32_t X, uint32_t lane) const {
-        const uint32_t q = X - 4 + 4 * lane;
-        return ld32(q < n - 4 ? q : n - 4);
+    LZ4E_DEV uint32_t ld32(uint32_t q) const { return buf_ld32(buf, vaddr(q)); }
+    LZ4E_DEV uint64_t ld64(uint32_t q) const {
+        const uint32_t v = vaddr(q);
+        return ((uint64_t)buf_ld32(buf, v + 4) << 32) | buf_ld32(buf, v);
     }
+    // Lanes past the block (or before it, X < 4) read 0 (range check) or a
+    // meaningless dword; every consumer masks those bytes.
+    LZ4E_DEV uint32_t stripe(uint32_t X, uint32_t lane) const { return ld32(X - 4 + 4 * lane); }
 };
 
 // A block staged in LDS as words (the last partial word zero-padded).
@@ -1151,7 +1153,7 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
     } else {
         block_sync();
         const uint8_t* base = in - D;
-        const HbmImage img{(gcu8*)base, D + n, buf_make(base, D + n)};
+        const HbmImage img{buf_make(base, D + n)};
         if (D != 0 && n >= kMinLength) {
             // LZ4_loadDict: every third dictionary position p with p + 8 <= D
             // (HASH_UNIT), in order -- the last put of a hash wins, so the

@@ -204,6 +204,10 @@ LZ4E_DEV ByteBuf buf_make(const void* p, uint32_t n) {
 LZ4E_DEV uint32_t buf_ld32(const ByteBuf& b, uint32_t q) {
     return __builtin_amdgcn_raw_buffer_load_b32(b.r, q, 0, 0);
 }
+// Byte at q (0 past the range).
+LZ4E_DEV uint32_t buf_ld8(const ByteBuf& b, uint32_t q) {
+    return __builtin_amdgcn_raw_buffer_load_b8(b.r, q, 0, 0);
+}
 #else
 struct ByteBuf {
     const uint8_t* p;
@@ -216,6 +220,7 @@ inline uint32_t buf_ld32(const ByteBuf& b, uint32_t q) {
     __builtin_memcpy(&v, b.p + q, 4);
     return v;
 }
+inline uint32_t buf_ld8(const ByteBuf& b, uint32_t q) { return q < b.n ? b.p[q] : 0u; }
 #endif
 typedef __attribute__((address_space(1))) const uint8_t gcu8;
 
