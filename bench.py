@@ -390,7 +390,10 @@ def block_floor(b: "Batch", top: int = 8, reps: int = 5) -> dict:
     time with the chip to themselves.  A stamped compress pass (per-block
     cycle counters, lz4e_debug_compress_stamped) names the `top` slowest
     blocks; each is then compressed and decoded alone (one-block launches,
-    HIP events on the batch's stream, best of `reps`).  However many GPUs
+    HIP events on the batch's stream, each pair right after a full-batch
+    compress so the lone wave runs at the clock the chip holds under this
+    workload, median of `reps`), and its stamped cycles alone are recorded
+    (a clock-free count).  However many GPUs
     share the corpus, a step cannot be shorter than this: strong scaling's
     ceiling is step(N=1) / floor."""
     import ctypes
