@@ -1950,10 +1950,17 @@ fail:
 struct CkState {
     int32_t wb, ob, fl, op;  // input window base, output window base, flushed prefix, output position
 };
+// The LDS the output side works in: the output window, the pointer-jumping
+// table of a batch's span, the store sink.
+struct CkOut {
+    lu8* W;
+    lu16* jump;
+    lu8* sink;  // a dword per lane
+};
 
 // Store output [fl, to) (to a multiple of 16, or exact when tail) from the window.
-LZ4E_DEV void ck_flush(CkLds& S, uint8_t* gout, CkState& C, int32_t to, bool tail, uint32_t lane) {
-    const lu8* W = (const lu8*)S.out;
+LZ4E_DEV void ck_flush(const CkOut& O, uint8_t* gout, CkState& C, int32_t to, bool tail, uint32_t lane) {
+    const lu8* W = O.W;
     const int32_t t16 = to & ~15;
     for (int32_t x = C.fl + 16 * (int32_t)lane; x < t16; x += 16 * (int32_t)kWave) {
         const u32x4 v = *(const lu128*)(W + (x - C.ob));
@@ -1973,8 +1980,8 @@ LZ4E_DEV int32_t ck_ob_for(const CkState& C, int32_t op) {
     return nob > C.ob ? nob : C.ob;
 }
 // Moves the output window forward to nob (> C.ob).
-LZ4E_DEV void ck_slide(CkLds& S, CkState& C, int32_t nob, uint32_t lane) {
-    lu8* W = (lu8*)S.out;
+LZ4E_DEV void ck_slide(const CkOut& O, CkState& C, int32_t nob, uint32_t lane) {
+    lu8* W = O.W;
     const int32_t d = nob - C.ob, end = (C.op + 15) & ~15;
     // forward in 1 KiB steps: step s writes [1024 s, +1024), reads d bytes
     // further on -- never a range an earlier step wrote
@@ -2048,6 +2055,27 @@ struct CkBatch {
     int32_t o = 0, L = 0, M = 0, lp = 0, off = 0, n0 = 0, nh = 0;
     uint4 h0 = {0, 0, 0, 0}, h1 = {0, 0, 0, 0};
 };
+// The part of each match whose source lies before the batch (lo): final,
+// from the window, or from HBM before B.ob (flushed: ob <= fl) -- those
+// loads issued here, consumed by ck_copy.
+LZ4E_DEV void ck_early(CkBatch& B, int32_t lo, const uint8_t* gout, uint32_t lane) {
+    const bool valid = (int32_t)lane < B.nf;
+    const int32_t m = B.o + B.L, ss = m - B.off, ob = B.ob;
+    int32_t n0 = 0, nh = 0;
+    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0;
+    if (valid && B.off != 0 && ss < lo) {
+        n0 = B.M < lo - ss ? B.M : lo - ss;
+        nh = ss < ob ? (n0 < ob - ss ? n0 : ob - ss) : 0;
+        if (nh > 0 && nh <= kCkLong) {
+            h0 = ldg16(gout + ss);
+            if (nh > 16) h1 = ldg16(gout + ss + 16);
+        }
+    }
+    B.n0 = n0;
+    B.nh = nh;
+    B.h0 = h0;
+    B.h1 = h1;
+}
 LZ4E_DEV void ck_fields(CkLds& S, int32_t wb, int32_t i, int32_t n, int32_t op, int32_t ob, int32_t iend,
                         int32_t oend, int32_t D, const uint8_t* gout, uint32_t lane, CkBatch& B) {
     const lu8* in = (const lu8*)S.in;
@@ -2084,31 +2112,17 @@ LZ4E_DEV void ck_fields(CkLds& S, int32_t wb, int32_t i, int32_t n, int32_t op, 
     B.M = M;
     B.lp = lp;
     B.off = off;
-    // the part of the match whose source lies before the batch: final, from
-    // the window, or from HBM before ob (flushed: ob <= fl)
-    const int32_t ss = m - off;
-    int32_t n0 = 0, nh = 0;
-    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0;
-    if (valid && off != 0 && ss < lo) {
-        n0 = M < lo - ss ? M : lo - ss;
-        nh = ss < ob ? (n0 < ob - ss ? n0 : ob - ss) : 0;
-        if (nh > 0 && nh <= kCkLong) {
-            h0 = ldg16(gout + ss);
-            if (nh > 16) h1 = ldg16(gout + ss + 16);
-        }
-    }
-    B.n0 = n0;
-    B.nh = nh;
-    B.h0 = h0;
-    B.h1 = h1;
+    (void)valid;
+    ck_early(B, lo, gout, lane);
 }
 
 // The copies of batch B into the output window (C.ob == B.ob).
+// (literal sources: in + lp, in LDS)
 template <bool kSt>
-LZ4E_DEV void ck_copy(CkLds& S, const CkBatch& B, int32_t oend, uint8_t* gout, uint32_t lane, CkSt& stp) {
-    const lu8* in = (const lu8*)S.in;
-    lu8* W = (lu8*)S.out;
-    lu8* sink = (lu8*)S.sink + 4 * lane;
+LZ4E_DEV void ck_copy(const CkOut& O, const lu8* in, const CkBatch& B, int32_t oend, uint8_t* gout,
+                      uint32_t lane, CkSt& stp) {
+    lu8* W = O.W;
+    lu8* sink = O.sink + 4 * lane;
     const bool valid = (int32_t)lane < B.nf;
     const int32_t ob = B.ob, lo = lane_val((uint32_t)B.o, 0), hi = B.hi;
     const int32_t o = B.o, L = B.L, M = B.M, lp = B.lp, off = B.off, n0 = B.n0, nh = B.nh;
@@ -2162,7 +2176,7 @@ LZ4E_DEV void ck_copy(CkLds& S, const CkBatch& B, int32_t oend, uint8_t* gout, u
         if (kCkPJ && np >= kCkPJMin && 4 * popc64(rm) <= np && !ballot(mine && m2 > 2 * kCkLong)) {
             if constexpr (kSt) stp.a[kCkNPJ]++;
             const int32_t s0 = (int32_t)lane_val((uint32_t)ms2, ctz64(pending)) - a0;
-            resolve_chains(span, (lu16*)S.jump, lo - a0, hi - a0, s0, mine, ms2 - a0, m2, off, lane);
+            resolve_chains(span, O.jump, lo - a0, hi - a0, s0, mine, ms2 - a0, m2, off, lane);
             break;
         }
         const bool lng = m2 > 2 * kCkLong;
@@ -2215,6 +2229,7 @@ LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* g
     const ByteBuf ib = buf_make(in - sh, (uint32_t)((srcSize + sh + 3) & ~3));
     const int32_t iend = srcSize, oend = outSize;
     CkState C{-sh, 0, 0, 0};
+    const CkOut O{(lu8*)S.out, (lu16*)S.jump, (lu8*)S.sink};
     bool wvalid = false;
     int32_t ip = 0, n = 0, i = 0, X = 0;
     bool stopped = false;
@@ -2236,7 +2251,7 @@ LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* g
                 i++;
                 exact = true;
             } else {
-                if (Bt.ob != C.ob) ck_slide(S, C, Bt.ob, lane);
+                if (Bt.ob != C.ob) ck_slide(O, C, Bt.ob, lane);
                 if constexpr (kSt) st.lap(kCkFlushSlide);
                 const int32_t i2 = i + Bt.nf;
                 if (kCkAhead && i2 < n)
@@ -2246,12 +2261,12 @@ LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* g
                     st.a[kCkBatches]++;
                     st.a[kCkSeqs] += (uint64_t)Bt.nf;
                 }
-                ck_copy<kSt>(S, Bt, oend, gout, lane, st);
+                ck_copy<kSt>(O, (const lu8*)S.in, Bt, oend, gout, lane, st);
                 if constexpr (kSt) st.lap(kCkCopy);
                 C.op = Bt.hi;
                 i = i2;
                 ip = C.wb + (i < n ? ck_pos(uni(((const lu32*)S.tok)[i])) : X);
-                if ((C.op & ~15) - C.fl >= kCkFlush) ck_flush(S, gout, C, C.op, false, lane);
+                if ((C.op & ~15) - C.fl >= kCkFlush) ck_flush(O, gout, C, C.op, false, lane);
                 if (i < n || !stopped) continue;
                 exact = true;  // the chain's stop: the exact path
                 n = 0;
@@ -2304,7 +2319,7 @@ LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* g
         if (exact) {
             if constexpr (kSt) st.lap(kCkFlushSlide);
             // every byte before op into HBM, then one sequence there
-            ck_flush(S, gout, C, C.op, true, lane);
+            ck_flush(O, gout, C, C.op, true, lane);
             wave_fence();
             bool done = false;
             int32_t op = C.op;
@@ -2359,6 +2374,188 @@ __global__ __launch_bounds__(64) void decompress_chunk_kernel(
 }
 constexpr uint32_t kCkPerCu = (160u * 1024u) / sizeof(CkLds);
 
+// ============================================================================
+// Relay decoder: a parser wave and a sequence-copier wave per block (mode 5)
+// ============================================================================
+//
+// Wave 0 parses exactly as the pipelined decoder does (parse_batch: the
+// reference's checks in its order, so the return value is decided there)
+// and publishes each batch -- per-lane records, output range and, for a
+// fast batch, the 512 input bytes of its parse window (the literals' source)
+// -- in a ring of record slots.  Wave 1 copies the batches in order into the
+// chunked decoder's LDS output window with its copy stage (ck_copy: whole
+// sequences per lane; the part of a match whose source lies before the batch
+// from the window, or from HBM before it; readiness rounds / pointer jumping
+// inside the batch), flushes the window to HBM 16 bytes per lane, and copies
+// a scalar-path batch (long runs, the block's final literals) in HBM after
+// flushing the whole window.  Every earlier batch is final when the copier
+// takes batch j -- one wave writes every output byte in order -- so there is
+// no cross-batch protocol beyond the record slots.  Waits are bounded by the
+// watchdog (LZ4E_DECODE_ABORTED), as in the pipelined decoder.
+#ifndef LZ4E_RELAY_RECS
+#define LZ4E_RELAY_RECS 4
+#endif
+constexpr uint32_t kRRecs = LZ4E_RELAY_RECS;
+enum { kRN, kRKind, kRLo, kRHi, kRBase, kRWords = 8 };
+struct RelayLds {
+    uint32_t ring[(kRing + kRingPad) / 4];  // parser input ring
+    int32_t rec[kRRecs][5][kWave];          // ls, L, op, off, M per sequence
+    int32_t hdr[kRRecs][kRWords];
+    uint32_t inp[kRRecs][2 * kWave];        // a fast batch's input window A|B (512 B)
+    uint8_t out[kCkOut + 16];               // output window
+    uint16_t jump[kCkCap + 32];             // pointer jumping over a batch's span
+    uint8_t sink[kSink];
+    int32_t pub[kRRecs], con[kRRecs];       // record slot published / consumed (batch index)
+    int32_t nb_total, abort, beat, result;
+};
+
+template <bool kStamps>
+__global__ __launch_bounds__(2 * kWave) void decompress_relay_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
+    const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
+    uint64_t* __restrict__ dbg, const int32_t* __restrict__ dict_len,
+    const uint32_t* __restrict__ order) {
+    __shared__ __attribute__((aligned(16))) RelayLds S;
+    if (blockIdx.x >= nblocks) return;
+    const uint32_t b = order ? order[blockIdx.x] : blockIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
+    const int32_t srcSize = src_len[b];
+    const int32_t outSize = dst_cap[b];
+    const uint8_t* in = src + src_off[b];
+    uint8_t* gout = dst + dst_off[b];
+    (void)dbg;
+    if (special_case(in, srcSize, outSize, ret + b, tid)) return;
+    if (tid < kRRecs) {
+        S.pub[tid] = -1;
+        S.con[tid] = (int32_t)tid - (int32_t)kRRecs;
+    }
+    if (tid == 0) {
+        S.nb_total = INT32_MAX;
+        S.abort = 0;
+        S.beat = 0;
+        S.result = kPipeAbort;
+    }
+    __syncthreads();
+
+    if (wave == 0) {
+        // ---------------- parser ----------------
+        __builtin_amdgcn_s_setprio(3);
+        Parse P;
+        P.init(in, srcSize, outSize, (lu32*)S.ring, lane, dict_of(dict_len, b));
+        int32_t j = 0;
+        for (;;) {
+            Batch bt;
+            const int32_t lo = P.op;
+            const ParseResult pr = parse_batch<true>(P, bt, lane, kCkCap);
+            if (pr == kParseFail) {
+                if (lane == 0) S.result = -P.ip - 1;
+                break;
+            }
+            const uint32_t slot = (uint32_t)j % kRRecs;
+            if (!wait_for(S, [&] { return lds_acquire(&S.con[slot]) == j - (int32_t)kRRecs; },
+                          [&] { return lds_acquire(&S.beat) + lds_acquire(&S.con[slot]); })) {
+                lds_release(&S.abort, 1);
+                break;
+            }
+            S.rec[slot][0][lane] = bt.ls;
+            S.rec[slot][1][lane] = bt.L;
+            S.rec[slot][2][lane] = bt.op;
+            S.rec[slot][3][lane] = bt.off;
+            S.rec[slot][4][lane] = bt.M;
+            if (pr == kParsedFast) {
+                S.inp[slot][lane] = P.win.a;
+                S.inp[slot][kWave + lane] = P.win.b;
+            }
+            if (lane < kRWords) {
+                const int32_t h[kRWords] = {(int32_t)bt.n, pr == kParsedScalar ? kKindHbm : kKindFast,
+                                            lo, P.op, P.win.base, 0, 0, 0};
+                int32_t v = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < kRWords; ++q) v = lane == q ? h[q] : v;
+                S.hdr[slot][lane] = v;
+            }
+            lds_release(&S.pub[slot], j);
+            j++;
+            if (P.done) {
+                if (lane == 0) S.result = P.op;
+                break;
+            }
+        }
+        lds_release(&S.nb_total, j);
+    } else {
+        // ---------------- copier ----------------
+        __builtin_amdgcn_s_setprio(2);
+        const CkOut O{(lu8*)S.out, (lu16*)S.jump, (lu8*)S.sink};
+        CkState C{0, 0, 0, 0};
+        CkSt st;
+        auto beat = [&] {
+            // (called in lane-divergent loops: lane 0 alone, no ordering)
+            if (lane == 0) __hip_atomic_fetch_add(&S.beat, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        };
+        for (int32_t j = 0;; ++j) {
+            const uint32_t slot = (uint32_t)j % kRRecs;
+            const bool ok = wait_for(
+                S, [&] { return lds_acquire(&S.pub[slot]) == j || lds_acquire(&S.nb_total) <= j; },
+                [&] { return lds_acquire(&S.beat) + lds_acquire(&S.pub[slot]); });
+            if (!ok) {
+                lds_release(&S.abort, 1);
+                break;
+            }
+            if (lds_acquire(&S.pub[slot]) != j) break;  // the parser ended before batch j
+            const int32_t ls = S.rec[slot][0][lane], L = S.rec[slot][1][lane], o = S.rec[slot][2][lane];
+            const int32_t off = S.rec[slot][3][lane], M = S.rec[slot][4][lane];
+            int32_t hdr[kRWords];
+#pragma unroll
+            for (uint32_t q = 0; q < kRWords; ++q) hdr[q] = (int32_t)uni((uint32_t)S.hdr[slot][q]);
+            const int32_t lo = hdr[kRLo], hi = hdr[kRHi];
+            if (hdr[kRKind] == kKindHbm) {
+                // every window byte into HBM, then the sequence in place
+                ck_flush(O, gout, C, C.op, true, lane);
+                wave_fence();
+                Batch bt;
+                bt.ls = ls;
+                bt.L = L;
+                bt.op = o;
+                bt.off = off;
+                bt.M = M;
+                bt.n = 1;
+                lds_release(&S.con[slot], j);
+                copy_scalar_hbm<4>(bt, in, srcSize, gout, outSize, lane, beat);
+                // the window restarts at the last 16-byte boundary
+                C.op = hi;
+                C.ob = C.fl = hi & ~15;
+                wave_fence();
+                if ((int32_t)lane < hi - C.ob) O.W[lane] = *(const gu8*)(gout + C.ob + lane);
+                lockstep();
+                continue;
+            }
+            CkBatch B;
+            B.i = j;
+            B.nf = hdr[kRN];
+            B.hi = hi;
+            B.ob = ck_ob_for(C, lo);
+            B.o = o;
+            B.L = L;
+            B.M = M;
+            B.lp = ls;
+            B.off = off;
+            if (B.ob != C.ob) ck_slide(O, C, B.ob, lane);
+            ck_early(B, lo, gout, lane);
+            ck_copy<false>(O, (const lu8*)S.inp[slot] - hdr[kRBase], B, outSize, gout, lane, st);
+            lds_release(&S.con[slot], j);
+            C.op = hi;
+            if ((C.op & ~15) - C.fl >= kCkFlush) ck_flush(O, gout, C, C.op, false, lane);
+        }
+        // (the final literals are a scalar-path batch: nothing is left in the window)
+        ck_flush(O, gout, C, C.op, true, lane);
+    }
+    __syncthreads();
+    if (tid == 0) ret[b] = __hip_atomic_load(&S.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                               ? kPipeAbort
+                               : S.result;
+}
+
 // Blocks whose capacity lies in [kPipeMinCap, kPipeMaxCap) take the
 // pipelined decoder.  Small blocks parse in a few batches, and one wave each
 // keeps more of them resident.  Large blocks (256 KiB: ~560 batches each)
@@ -2394,9 +2591,29 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
     static const char* env = getenv("LZ4E_DECOMPRESS_MODE");
     uint32_t mode = a.mode;
     if (mode == kDecAuto && env)
-        mode = env[0] == 'w' ? kDecWave : (env[0] == 'p' ? kDecPipe : (env[0] == 'c' ? kDecChunk : kDecAuto));
+        mode = env[0] == 'w' ? kDecWave
+                             : (env[0] == 'p' ? kDecPipe
+                                              : (env[0] == 'c' ? kDecChunk : (env[0] == 'r' ? kDecRelay : kDecAuto)));
     if (mode == kDecAuto)
         mode = (a.max_cap == 0 || (a.max_cap >= kPipeMinCap && a.max_cap < kPipeMaxCap)) ? kDecPipe : kDecWave;
+    if (mode == kDecRelay) {
+        const int om = launch_order_mode(false);
+        uint32_t* order = nullptr;
+        if ((om == kOrderAlways || (om == kOrderAuto && a.nblocks > 256 * ((160u * 1024u) / sizeof(RelayLds)))) &&
+            hipMallocAsync((void**)&order, sizeof(uint32_t) * a.nblocks, stream) == hipSuccess) {
+            hipLaunchKernelGGL((order_kernel<DecodeWeight>), dim3(1), dim3(kOrderThreads), 0, stream,
+                               DecodeWeight{a.src_len, a.dst_cap}, a.nblocks, order);
+        } else {
+            (void)hipGetLastError();
+            order = nullptr;
+        }
+        hipLaunchKernelGGL((decompress_relay_kernel<kStamps>), dim3(a.nblocks), dim3(2 * kWave), 0, stream,
+                           a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
+                           dbg, a.dict_len, (const uint32_t*)order);
+        const hipError_t err = hipGetLastError();
+        if (order) (void)hipFreeAsync(order, stream);
+        return err;
+    }
     if (mode == kDecChunk) {
         const int om = launch_order_mode(false);
         uint32_t* order = nullptr;

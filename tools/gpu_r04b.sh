@@ -26,5 +26,5 @@ for w in fio4k sg512 text256k; do
   step bench_$w 600 python -u bench.py --workload $w --steps 5 --warmup 2 --no-single-call
 done
 LZ4E_COMPRESS_LDS_MAX=0 step bench_fio4k_hbm_input 600 python -u bench.py --workload fio4k --steps 5 --warmup 2 --no-single-call --no-e2e --no-cpu-baseline --no-strong
-step decmodes 400 python -u tools/decmodes.py 2,1,4 classes,silesia,text256k,fio4k
+step decmodes 400 python -u tools/decmodes.py 2,1,5,4 classes,silesia,text256k,fio4k
 echo done >&2
