@@ -252,11 +252,12 @@ def _emu_decode_pipe(exe, tmp_path, frame, cap, dic=b"", flag="-p"):
 PIPE_CASES = [(k, m) for k in ("text", "records", "ints", "runs") for m in range(5)] + [("random", 0)]
 
 
-@pytest.mark.parametrize("flag", ["-p", "-c"], ids=["pipe", "chunk"])
+@pytest.mark.parametrize("flag", ["-p", "-c", "-r"], ids=["pipe", "chunk", "relay"])
 @pytest.mark.parametrize("kind,mode", PIPE_CASES, ids=[f"{k}-{m}" for k, m in PIPE_CASES])
 def test_emulated_pipe_decoder_sanitized(emu_exe, tmp_path, kind, mode, flag):
-    """The 4-wave pipelined decoder (-p) and the one-wave chunked decoder (-c:
-    speculative token walks, LDS output window, HBM far sources)
+    """The 4-wave pipelined decoder (-p), the one-wave chunked decoder (-c:
+    speculative token walks, LDS output window, HBM far sources) and the
+    2-wave relay decoder (-r: parser wave + sequence copier wave)
     on 16-64 KiB blocks: valid frames (mode 0), truncations (1), bit flips
     (2), short capacity (3) and a dictionary (4): values, error codes and
     bytes equal the oracle's (/root/reference/lz4e/lz4e_decompress.c:62-460
@@ -292,7 +293,7 @@ def emu_exe_spin1(tmp_path_factory):
     shutil.rmtree(b, ignore_errors=True)
 
 
-@pytest.mark.parametrize("flag", ["-p"], ids=["pipe"])
+@pytest.mark.parametrize("flag", ["-p", "-r"], ids=["pipe", "relay"])
 def test_emulated_pipe_decoder_watchdog(emu_exe_spin1, tmp_path, flag):
     """A forced watchdog: every wave leaves its loop (the run ends), the
     block's value is LZ4E_DECODE_ABORTED -- even though the parser itself

@@ -72,7 +72,7 @@ def _gpu_compress(amd, blocks, ttypes, caps=None):
     return r, frames, ax
 
 
-DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_CHUNK = 0, 1, 2, 4
+DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_CHUNK, DEC_RELAY = 0, 1, 2, 4, 5
 
 
 def _gpu_decompress(amd, frames, caps, csizes=None, max_cap=None, mode=DEC_AUTO):
@@ -276,7 +276,8 @@ def test_decompress_batch_vs_oracle(gpu, kind):
         assert outs[i] == eo == expect[i]
 
 
-@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_CHUNK, DEC_PIPE, DEC_WAVE], ids=["auto", "chunk", "pipe", "wave"])
+@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_CHUNK, DEC_RELAY, DEC_PIPE, DEC_WAVE],
+                         ids=["auto", "chunk", "relay", "pipe", "wave"])
 @pytest.mark.parametrize("mode", ["truncate", "flip", "garbage", "small_cap", "csize"])
 def test_decompress_error_codes(gpu, mode, dec):
     rng = np.random.default_rng(1234 + len(mode))
@@ -342,7 +343,7 @@ def test_full_size_roundtrip(gpu, cls, bs, kind):
         assert frames[i] == oracle_ref.compress(blocks[i], cls)[1]
 
 
-@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_CHUNK], ids=["wave", "pipe", "chunk"])
+@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_CHUNK, DEC_RELAY], ids=["wave", "pipe", "chunk", "relay"])
 def test_decompress_huge_runs(gpu, mode):
     """Blocks whose sequences are hundreds of MiB long: a 256 MiB run of one
     byte (a single match whose length extension is ~1 MiB of 0xFF) and a
@@ -361,7 +362,7 @@ def test_decompress_huge_runs(gpu, mode):
         assert outs[i] == b, i
 
 
-@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_CHUNK], ids=["wave", "pipe", "chunk"])
+@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_CHUNK, DEC_RELAY], ids=["wave", "pipe", "chunk", "relay"])
 @pytest.mark.parametrize("cap_extra", [0, 100000])
 def test_decompress_periodic_matches(gpu, cap_extra, mode):
     """Self-overlapping matches of every period 1..40 and lengths around
@@ -707,8 +708,9 @@ def test_full_size_sg512_layout_every_frame(gpu):
 
 @pytest.mark.parametrize("kind", ["mixed", "text", "runs", "ints", "random", "small_alpha", "fio"])
 def test_decompress_pipelined_vs_wave_decoder(gpu, kind):
-    """The three decoders on the same frames -- the pipelined 4-wave decoder,
-    the one-wave chunked decoder and the one-wave decoder -- valid frames,
+    """The four decoders on the same frames -- the pipelined 4-wave decoder,
+    the relay decoder, the one-wave chunked decoder and the one-wave decoder
+    -- valid frames,
     exact and spare capacities, and corrupted ones: identical values and
     bytes, all equal to the oracle's."""
     rng = np.random.default_rng(zlib.crc32(kind.encode()))
@@ -738,10 +740,11 @@ def test_decompress_pipelined_vs_wave_decoder(gpu, kind):
     r_wg, o_wg = _gpu_decompress(gpu, frames, caps, mode=DEC_PIPE)
     r_wv, o_wv = _gpu_decompress(gpu, frames, caps, mode=DEC_WAVE)
     r_ck, o_ck = _gpu_decompress(gpu, frames, caps, mode=DEC_CHUNK)
+    r_rl, o_rl = _gpu_decompress(gpu, frames, caps, mode=DEC_RELAY)
     for i, (er, eb) in enumerate(want):
-        assert r_wg[i] == er == r_wv[i] == r_ck[i], (i, r_wg[i], er, r_wv[i], r_ck[i])
+        assert r_wg[i] == er == r_wv[i] == r_ck[i] == r_rl[i], (i, r_wg[i], er, r_wv[i], r_ck[i], r_rl[i])
         if er >= 0:
-            assert o_wg[i] == eb == o_wv[i] == o_ck[i], i
+            assert o_wg[i] == eb == o_wv[i] == o_ck[i] == o_rl[i], i
 
 
 # ---------------------------------------------------------------------------
