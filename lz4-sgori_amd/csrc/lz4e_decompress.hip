@@ -173,6 +173,9 @@ struct InWindow {
         return ld4(reinterpret_cast<const lu8*>(ring) + ((uint32_t)(p + shift) & (kRing - 1)));
     }
     LZ4E_DEV uint32_t rd16(int32_t p) const { return rd4(p) & 0xFFFFu; }
+    // Block bytes [p, p + n) all held by the ring (at ring offsets that may
+    // wrap: see wave_lit_ring).
+    LZ4E_DEV bool holds(int32_t p, int32_t n) const { return p >= ring_lo && p + n <= base + 512; }
     // The ring copy of block bytes [p, p + n), or nullptr when not all held.
     LZ4E_DEV const lu8* in_ring(int32_t p, int32_t n) const {
         if (p < ring_lo || p + n > base + 512) return nullptr;
@@ -820,16 +823,115 @@ LZ4E_DEV void copy_scalar_hbm(const Batch& b, const uint8_t* in, int32_t srcSize
     wave_fence();
 }
 
+// ---------------------------------------------------------------- small blocks in LDS
+// A block of at most kSmallOut output bytes without a dictionary (4 KiB
+// blocks, the drop-in single calls) can keep its whole output in LDS: a
+// scalar-path sequence (long literal runs and matches, as in fio-style
+// data) then copies LDS to LDS at LDS latency instead of a store, a load
+// that waits behind it and another store in HBM per sequence, and the block
+// leaves in one pass of 16-byte stores at the end.
+constexpr int32_t kSmallOut = 4608;  // 4 KiB blocks and their 4 KiB + 32 capacities
+constexpr uint32_t kSmallBuf = kSmallOut + 64;
+
+// Whole-wave copy of n (<= 1024 per call of a round) bytes of a literal run
+// from the input ring (block bytes [p, p + n) held by it): 16 bytes per lane,
+// ring offsets wrap through the mirror.
+LZ4E_DEV void wave_lit_ring(lu8* dst, const InWindow& w, int32_t p, int32_t n, lu8* sink,
+                            uint32_t lane) {
+    const lu8* r = reinterpret_cast<const lu8*>(w.ring);
+    for (int32_t k = 16 * (int32_t)lane; k < n; k += 16 * (int32_t)kWave)
+        piece16(dst + k, r + ((uint32_t)(p + w.shift + k) & (kRing - 1)),
+                (uint32_t)(n - k < 16 ? n - k : 16), sink);
+}
+
+// Whole-wave copy of n (<= kSmallOut) literal bytes from HBM into LDS: every
+// load before the first store (one round trip); loads never read at or past
+// srcSize.
+LZ4E_DEV void wave_lit_hbm(lu8* dst, const uint8_t* in, int32_t p, int32_t n, int32_t srcSize,
+                           lu8* sink, uint32_t lane) {
+    constexpr int kR = (kSmallOut + 16 * kWave - 1) / (16 * kWave);
+    uint4 v[kR];
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+        const int32_t k = 16 * ((int32_t)lane + j * (int32_t)kWave);
+        v[j] = (k < n && p + k + 16 <= srcSize) ? ldg16(in + p + k) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < kR; ++j) {
+        const int32_t k = 16 * ((int32_t)lane + j * (int32_t)kWave);
+        if (k >= n) continue;
+        const int32_t c = n - k < 16 ? n - k : 16;
+        if (p + k + 16 <= srcSize) put16(dst + k, v[j], (uint32_t)c, sink);
+        else
+            for (int32_t t = 0; t < c; ++t) dst[k + t] = in[p + k + t];
+    }
+}
+
+// Whole-wave match copy inside LDS: out[op + t] = out[op + t - off] for t in
+// [0, len), any overlap (offset 0: zeros).  Round r copies [t, t + c) from D
+// bytes back, D a multiple of off with c <= D <= t + off, so every source
+// byte is final before the round; D doubles while 2D <= t (a run of period
+// 1 takes ~log2(len) rounds).  The loop is wave-uniform.
+LZ4E_DEV void wave_match_lds(lu8* out, int32_t op, uint32_t off, int32_t len, lu8* sink,
+                             uint32_t lane) {
+    if (off == 0) {
+        for (int32_t k = 16 * (int32_t)lane; k < len; k += 16 * (int32_t)kWave)
+            put16(out + op + k, make_uint4(0, 0, 0, 0), (uint32_t)(len - k < 16 ? len - k : 16), sink);
+        return;
+    }
+    int32_t t = 0, D = (int32_t)off;
+    while (t < len) {
+        int32_t c = len - t < D ? len - t : D;
+        c = c < 16 * (int32_t)kWave ? c : 16 * (int32_t)kWave;
+        lu8* d = out + op + t;
+        const int32_t k = 16 * (int32_t)lane;
+        if (k < c) piece16(d + k, d + k - D, (uint32_t)(c - k < 16 ? c - k : 16), sink);
+        lockstep();  // the next round reads these bytes
+        t += c;
+        while (2 * D <= t) D *= 2;
+    }
+}
+
+// Copies of a scalar-path batch (one sequence, any length) into the LDS
+// output: the literal run from the input ring when it holds it, else from
+// HBM, then the match.
+LZ4E_DEV void copy_scalar_lds(const Batch& b, const InWindow& win, const uint8_t* in,
+                              int32_t srcSize, lu8* obuf, lu8* sink, uint32_t lane) {
+    const int32_t L = lane_val((uint32_t)b.L, 0), op = lane_val((uint32_t)b.op, 0);
+    const int32_t ls = lane_val((uint32_t)b.ls, 0);
+    const int32_t M = lane_val((uint32_t)b.M, 0), off = lane_val((uint32_t)b.off, 0);
+    if (L > 0) {
+        if (win.holds(ls, L) && L <= 16 * (int32_t)kWave) wave_lit_ring(obuf + op, win, ls, L, sink, lane);
+        else wave_lit_hbm(obuf + op, in, ls, L, srcSize, sink, lane);
+        lockstep();
+    }
+    if (M > 0) wave_match_lds(obuf, op + L, (uint32_t)off, M, sink, lane);
+}
+
+// The LDS output [0, n) to HBM in 16-byte stores (the partial end chunk by
+// bytes: nothing past n is written).
+LZ4E_DEV void flush_lds(uint8_t* gout, const lu8* obuf, int32_t n, uint32_t lane) {
+    for (int32_t c0 = 16 * (int32_t)lane; c0 < n; c0 += 16 * (int32_t)kWave) {
+        const lu8* sc = obuf + c0;
+        if (c0 + 16 <= n) stg16(gout + c0, make_uint4(ld4(sc), ld4(sc + 4), ld4(sc + 8), ld4(sc + 12)));
+        else
+            for (int32_t x = c0; x < n; ++x) *(gu8*)(gout + x) = sc[x - c0];
+    }
+}
+
 struct Stamps {
     uint64_t t = 0, acc[4] = {0, 0, 0, 0}, batches = 0, rounds = 0;
 };
 
 // Decode one block into HBM on one wave.  LDS: the input ring, the store
-// sink, the span buffer of the fast batches and its jump table.
-template <bool kStamps>
+// sink, the span buffer of the fast batches and its jump table.  kLdsOut:
+// the whole output is assembled in obuf (kSmallBuf bytes; outSize <=
+// kSmallOut, no dictionary) and stored at the end; a fast batch's span is
+// then obuf itself.
+template <bool kStamps, bool kLdsOut = false>
 LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, int32_t outSize,
-                           int32_t* ret_slot, uint64_t* dbg, uint32_t lane, lu8* span,
-                           lu32* ring, lu16* jump, int32_t dict) {
+                           int32_t* ret_slot, uint64_t* dbg, uint32_t lane, lu8* span_buf,
+                           lu32* ring, lu16* jump, int32_t dict, lu8* obuf = nullptr) {
     Stamps st;
     auto lap = [&](int ph) {
         if constexpr (kStamps) {
@@ -862,20 +964,26 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
             // the rest in LDS dependency rounds.  Then one store pass.
             const int32_t lo = lane_val((uint32_t)b.op, 0);
             const int32_t a0 = lo & ~15;  // span index of position x: x - a0
+            lu8* span = kLdsOut ? obuf + a0 : span_buf;
             const int32_t ms = b.op + b.L, ss = ms - b.off;
             int32_t n0 = 0;
             uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0;
             if (valid && ss < lo) {  // fast path: lo <= oend - 32, so [ss, ss + 32) is in the block
                 n0 = b.M < lo - ss ? b.M : lo - ss;
-                h0 = ldg16(gout + ss);
-                if (n0 > 16) h1 = ldg16(gout + ss + 16);
+                if constexpr (!kLdsOut) {
+                    h0 = ldg16(gout + ss);
+                    if (n0 > 16) h1 = ldg16(gout + ss + 16);
+                }
             }
             if (valid && b.L > 0) {
                 const lu8* rs = P.win.in_ring(b.ls, b.L);
                 if (rs) lane_copy(span + (b.op - a0), rs, b.L, sink);
                 else lane_copy64(span + (b.op - a0), in + b.ls, b.L, in + srcSize);
             }
-            if (n0 > 0) {
+            if constexpr (kLdsOut) {
+                // the source bytes before lo are final in obuf (and end before ms)
+                if (n0 > 0) lane_copy(span + (ms - a0), obuf + ss, n0, sink);
+            } else if (n0 > 0) {
                 put16(span + (ms - a0), h0, n0 < 16 ? n0 : 16, sink);
                 if (n0 > 16) put16(span + (ms - a0) + 16, h1, n0 - 16, sink);
             }
@@ -911,7 +1019,7 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
             lap(2);
             lockstep();  // the last round's span bytes, read by other lanes
             // store pass: 16-byte HBM chunks of [lo, op); partial end chunks by bytes
-            const int32_t nch = (op - a0 + 15) >> 4;
+            const int32_t nch = kLdsOut ? 0 : (op - a0 + 15) >> 4;
             for (int32_t i = (int32_t)lane; i < nch; i += kWave) {
                 const int32_t c0 = a0 + 16 * i;
                 const lu8* sc = span + 16 * i;
@@ -925,7 +1033,12 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
             lap(3);
         } else {
             // ---------------- in-HBM copies (scalar-path batches) -----------
-            copy_scalar_hbm(b, in, srcSize, gout, outSize, lane);
+            if constexpr (kLdsOut) {
+                copy_scalar_lds(b, P.win, in, srcSize, obuf, sink, lane);
+                lockstep();  // later batches read these bytes
+            } else {
+                copy_scalar_hbm(b, in, srcSize, gout, outSize, lane);
+            }
             lap(2);
         }
         if (P.done) {
@@ -933,6 +1046,9 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
             break;
         }
     }
+    // (a failed block leaves the output its completed batches wrote, as the
+    // HBM form does)
+    if constexpr (kLdsOut) flush_lds(gout, obuf, P.op, lane);
     if constexpr (kStamps) {
         if (lane == 0 && dbg) {
             dbg[0] = st.acc[0];
@@ -973,7 +1089,9 @@ LZ4E_DEV bool special_case(const uint8_t* in, int32_t srcSize, int32_t outSize, 
     return false;
 }
 
-template <bool kStamps>
+// kSmall: the LDS-output form for blocks of at most kSmallOut bytes without
+// a dictionary (other blocks of the launch take the HBM form).
+template <bool kStamps, bool kSmall = false>
 __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restrict__ src,
                                                         const uint64_t* __restrict__ src_off,
                                                         const int32_t* __restrict__ src_len,
@@ -992,11 +1110,17 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
     uint8_t* out = dst + dst_off[b];
     uint64_t* d = kStamps && dbg ? dbg + 8 * (size_t)b : nullptr;
     if (special_case(in, srcSize, outSize, ret + b, lane)) return;
-    // LDS: [input ring + mirror] [store sink] [span] [jump table]
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kRing + kRingPad + kSink + kSpan + kJump];
-    decode_block<kStamps>(in, srcSize, out, outSize, ret + b, d, lane,
-                          (lu8*)(smem + kRing + kRingPad + kSink), (lu32*)smem,
-                          (lu16*)(smem + kRing + kRingPad + kSink + kSpan), dict_of(dict_len, b));
+    // LDS: [input ring + mirror] [store sink] [span | small-block output] [jump table]
+    constexpr uint32_t kMid = kSmall ? kSmallBuf : kSpan;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kRing + kRingPad + kSink + kMid + kJump];
+    lu8* mid = (lu8*)(smem + kRing + kRingPad + kSink);
+    lu16* jump = (lu16*)(smem + kRing + kRingPad + kSink + kMid);
+    const int32_t dict = dict_of(dict_len, b);
+    if (kSmall && dict == 0 && outSize <= kSmallOut)
+        decode_block<kStamps, true>(in, srcSize, out, outSize, ret + b, d, lane, mid, (lu32*)smem, jump,
+                                    0, mid);
+    else
+        decode_block<kStamps>(in, srcSize, out, outSize, ret + b, d, lane, mid, (lu32*)smem, jump, dict);
 }
 
 // ============================================================================
@@ -2594,8 +2718,11 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
         mode = env[0] == 'w' ? kDecWave
                              : (env[0] == 'p' ? kDecPipe
                                               : (env[0] == 'c' ? kDecChunk : (env[0] == 'r' ? kDecRelay : kDecAuto)));
+    if (mode == kDecAuto && env && env[0] == 's') mode = kDecSmall;
     if (mode == kDecAuto)
-        mode = (a.max_cap == 0 || (a.max_cap >= kPipeMinCap && a.max_cap < kPipeMaxCap)) ? kDecPipe : kDecWave;
+        mode = (a.max_cap == 0 || (a.max_cap >= kPipeMinCap && a.max_cap < kPipeMaxCap))
+                   ? kDecPipe
+                   : (a.max_cap <= (uint32_t)kSmallOut ? kDecSmall : kDecWave);
     if (mode == kDecRelay) {
         const int om = launch_order_mode(false);
         uint32_t* order = nullptr;
@@ -2650,9 +2777,14 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
         if (order) (void)hipFreeAsync(order, stream);
         return err;
     }
-    hipLaunchKernelGGL((decompress_kernel<kStamps>), dim3(a.nblocks), dim3(kWave), 0, stream,
-                       a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
-                       dbg, a.dict_len);
+    if (mode == kDecSmall)
+        hipLaunchKernelGGL((decompress_kernel<kStamps, true>), dim3(a.nblocks), dim3(kWave), 0, stream,
+                           a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
+                           dbg, a.dict_len);
+    else
+        hipLaunchKernelGGL((decompress_kernel<kStamps>), dim3(a.nblocks), dim3(kWave), 0, stream,
+                           a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
+                           dbg, a.dict_len);
     return hipGetLastError();
 }
 

@@ -74,11 +74,7 @@ struct HostBuf {
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
-        // coherent (fine-grained) and mapped: kernels read small batches'
-        // inputs straight from it, so no GPU cache may hold a stale copy of
-        // bytes the host rewrote for the next call
-        if (!hip_ok(hipHostMalloc(&p, want, hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"))
-            return false;
+        if (!hip_ok(hipHostMalloc(&p, want, hipHostMallocDefault), "hipHostMalloc")) return false;
         cap = want;
         return true;
     }
@@ -285,15 +281,6 @@ int table_type_of(const struct bio_vec* bv, const struct bvec_iter* it) {
     return tt;
 }
 
-// Batches small enough to run straight from / into pinned host memory (the
-// kernels' device view of it): no H2D copy, no copy-back kernels.
-constexpr uint32_t kDirectMaxBlocks = 16;
-constexpr uint64_t kDirectMaxBytes = 1ull << 20;
-bool direct_ok(uint32_t blocks, uint64_t bytes) {
-    static const bool off = getenv("LZ4E_NO_DIRECT") != nullptr;  // A/B: staged path only
-    return !off && blocks <= kDirectMaxBlocks && bytes <= kDirectMaxBytes;
-}
-
 // Descriptor block of a batch of R blocks, at `base` inside a staging
 // buffer: the inputs the kernels read, then the results they write.
 struct MetaLayout {
@@ -395,13 +382,7 @@ int compress_sg_batch_impl(struct lz4e_sg_request* reqs, int n, const char* cons
         reinterpret_cast<uint32_t*>(hd + m.dst_cap)[j] = q.dstIter->bi_size;
         reinterpret_cast<uint32_t*>(hd + m.dict_len)[j] = dl[j];
     }
-    // Small batches (the drop-in single call): the kernel reads its inputs
-    // and writes frames and results straight through the pinned buffer's
-    // device mapping -- blocks of <= kMaxLdsInput bytes are staged into LDS
-    // with one burst of loads, so PCIe latency is paid once -- and there is
-    // no H2D copy and no copy-back kernel: a launch and a sync.
-    const bool direct = direct_ok(L, fbase + f) && max_len <= lz4e::kMaxLdsInput;
-    uint8_t* dd = static_cast<uint8_t*>(direct ? c.h_dev : c.d.p);
+    uint8_t* dd = static_cast<uint8_t*>(c.d.p);
     lz4e::CompressBatch a{dd,
                           reinterpret_cast<const uint64_t*>(dd + m.src_off),
                           reinterpret_cast<const uint32_t*>(dd + m.src_len),
@@ -414,23 +395,17 @@ int compress_sg_batch_impl(struct lz4e_sg_request* reqs, int n, const char* cons
                           L,
                           max_len};
     if (dicts) a.dict_len = reinterpret_cast<const uint32_t*>(dd + m.dict_len);
-    if (direct) {
-        if (!hip_ok(lz4e::launch_compress(a, c.stream), "compress launch") ||
-            !hip_ok(hipStreamSynchronize(c.stream), "compress sync"))
-            return -1;
-    } else {
-        if (!hip_ok(hipMemcpyAsync(dd, hd, m.ret, hipMemcpyHostToDevice, c.stream), "H2D") ||
-            !hip_ok(lz4e::launch_compress(a, c.stream), "compress launch") ||
-            !hip_ok(copy_flat(c.h_dev, dd, m.ret, m.total - m.ret, c.stream), "copy-back meta"))
-            return -1;
-        hipLaunchKernelGGL(copy_blocks_kernel, dim3(L), dim3(256), 0, c.stream, dd,
-                           static_cast<uint8_t*>(c.h_dev),
-                           reinterpret_cast<const uint64_t*>(dd + m.dst_off),
-                           reinterpret_cast<const int32_t*>(dd + m.ret), L);
-        if (!hip_ok(hipGetLastError(), "copy-back frames") ||
-            !hip_ok(hipStreamSynchronize(c.stream), "compress sync"))
-            return -1;
-    }
+    if (!hip_ok(hipMemcpyAsync(dd, hd, m.ret, hipMemcpyHostToDevice, c.stream), "H2D") ||
+        !hip_ok(lz4e::launch_compress(a, c.stream), "compress launch") ||
+        !hip_ok(copy_flat(c.h_dev, dd, m.ret, m.total - m.ret, c.stream), "copy-back meta"))
+        return -1;
+    hipLaunchKernelGGL(copy_blocks_kernel, dim3(L), dim3(256), 0, c.stream, dd,
+                       static_cast<uint8_t*>(c.h_dev),
+                       reinterpret_cast<const uint64_t*>(dd + m.dst_off),
+                       reinterpret_cast<const int32_t*>(dd + m.ret), L);
+    if (!hip_ok(hipGetLastError(), "copy-back frames") ||
+        !hip_ok(hipStreamSynchronize(c.stream), "compress sync"))
+        return -1;
     int ok = 0;
     for (uint32_t j = 0; j < L; ++j) {
         lz4e_sg_request& q = reqs[map[j]];
@@ -689,11 +664,7 @@ int decompress_batch_impl(const char* const* src, const int* csize, char* const*
         reinterpret_cast<int32_t*>(hd + m_dl)[i] = dl[i];
         if (dl[i]) std::memcpy(hd + dso[i] - dl[i], dicts[i] + dict_sizes[i] - dl[i], (size_t)dl[i]);
     }
-    // small batches: straight through the pinned buffer's device mapping
-    // (see compress_sg_batch_impl); the chunked decoder reads each frame in
-    // 1 KiB bursts and keeps a 4 KiB block's output in LDS until it flushes
-    const bool direct = direct_ok(R, obase + d);
-    uint8_t* dd = static_cast<uint8_t*>(direct ? c.h_dev : c.d.p);
+    uint8_t* dd = static_cast<uint8_t*>(c.d.p);
     lz4e::DecompressBatch a{dd,
                             reinterpret_cast<const uint64_t*>(dd + m_so),
                             reinterpret_cast<const int32_t*>(dd + m_sl),
@@ -704,21 +675,11 @@ int decompress_batch_impl(const char* const* src, const int* csize, char* const*
                             R,
                             (uint32_t)std::max(0, *std::max_element(cap, cap + n))};
     if (dicts) a.dict_len = reinterpret_cast<const int32_t*>(dd + m_dl);
-    // (the chunked decoder keeps a small block's output in LDS until it
-    // flushes it, so no match source is read back over PCIe)
-    static const bool mode_env = getenv("LZ4E_DECOMPRESS_MODE") != nullptr;
-    if (direct && !mode_env) a.mode = lz4e::kDecChunk;
     const uint64_t h2d = dicts ? obase + d : m_rt;  // the dictionaries live among the outputs
-    bool ok;
-    if (direct) {
-        ok = hip_ok(lz4e::launch_decompress(a, c.stream), "decompress launch") &&
-             hip_ok(hipStreamSynchronize(c.stream), "decompress sync");
-    } else {
-        ok = hip_ok(hipMemcpyAsync(dd, hd, h2d, hipMemcpyHostToDevice, c.stream), "H2D") &&
-             hip_ok(lz4e::launch_decompress(a, c.stream), "decompress launch") &&
-             hip_ok(copy_flat(c.h_dev, dd, m_rt, 4ull * R, c.stream), "copy-back ret");
-    }
-    if (ok && !direct) {
+    bool ok = hip_ok(hipMemcpyAsync(dd, hd, h2d, hipMemcpyHostToDevice, c.stream), "H2D") &&
+              hip_ok(lz4e::launch_decompress(a, c.stream), "decompress launch") &&
+              hip_ok(copy_flat(c.h_dev, dd, m_rt, 4ull * R, c.stream), "copy-back ret");
+    if (ok) {
         hipLaunchKernelGGL(copy_blocks_kernel, dim3(R), dim3(256), 0, c.stream, dd,
                            static_cast<uint8_t*>(c.h_dev),
                            reinterpret_cast<const uint64_t*>(dd + m_do),

@@ -174,6 +174,42 @@ def test_emulated_decoder_sanitized(emu_exe, tmp_path, kind, mode, flag):
             assert got[1] == want[1], rep
 
 
+SMALL_CASES = [(k, m) for k in ("text", "records", "runs", "random", "fio") for m in range(5)]
+
+
+@pytest.mark.parametrize("kind,mode", SMALL_CASES, ids=[f"{k}-{m}" for k, m in SMALL_CASES])
+def test_emulated_small_block_decoder_sanitized(emu_exe, tmp_path, kind, mode):
+    """The one-wave decoder's LDS-output form (blocks of <= 4608 bytes, the
+    whole output assembled in LDS, scalar-path sequences copied LDS to LDS):
+    valid frames (mode 0), truncations (1), bit flips (2), short capacity (3)
+    and a dictionary (4: such blocks take the HBM form) equal the oracle."""
+    rng = np.random.default_rng(500 + mode)
+    for rep in range(4):
+        n = int(rng.choice([4096, int(rng.integers(13, 4609))]))
+        if kind == "fio":  # fio-style 4 KiB buffers: long literal runs and long matches
+            fio = corpus.fio_pattern(16 * 4096)
+            data = fio[(rep + 2) * 4096 - 9000:][:n + 9000].tobytes()
+        else:
+            data = _block(kind, n + 9000, 11 + rep + n).tobytes()
+        dic, blk = (data[:9000], data[9000:]) if mode == 4 else (b"", data[:n])
+        f = oracle_ref.compress_dict(blk, dic)[1] if mode == 4 else oracle_ref.compress(blk, BYU16)[1]
+        cap = len(blk) + (32 if rep == 1 else 0)
+        if mode == 1:
+            f = f[:int(rng.integers(1, len(f)))]
+        elif mode == 2:
+            fb = bytearray(f)
+            for _ in range(3):
+                fb[int(rng.integers(0, len(fb)))] ^= 1 << int(rng.integers(0, 8))
+            f = bytes(fb)
+        elif mode == 3:
+            cap = max(0, len(blk) - int(rng.integers(1, 40)))
+        want = oracle_ref.decompress_dict(f, cap, dic)
+        got = _emu_decode(emu_exe, tmp_path, f, cap, dic, "-l")
+        assert got[0] == want[0], (rep, got[0], want[0])
+        if want[0] >= 0:
+            assert got[1] == want[1], rep
+
+
 VEC_CASES = [(k, m) for k in ("random", "runs", "text") for m in range(4)]
 
 

@@ -72,7 +72,7 @@ def _gpu_compress(amd, blocks, ttypes, caps=None):
     return r, frames, ax
 
 
-DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_CHUNK, DEC_RELAY = 0, 1, 2, 4, 5
+DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_CHUNK, DEC_RELAY, DEC_SMALL = 0, 1, 2, 4, 5, 6
 
 
 def _gpu_decompress(amd, frames, caps, csizes=None, max_cap=None, mode=DEC_AUTO):
@@ -276,8 +276,8 @@ def test_decompress_batch_vs_oracle(gpu, kind):
         assert outs[i] == eo == expect[i]
 
 
-@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_CHUNK, DEC_RELAY, DEC_PIPE, DEC_WAVE],
-                         ids=["auto", "chunk", "relay", "pipe", "wave"])
+@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_CHUNK, DEC_RELAY, DEC_PIPE, DEC_WAVE, DEC_SMALL],
+                         ids=["auto", "chunk", "relay", "pipe", "wave", "small"])
 @pytest.mark.parametrize("mode", ["truncate", "flip", "garbage", "small_cap", "csize"])
 def test_decompress_error_codes(gpu, mode, dec):
     rng = np.random.default_rng(1234 + len(mode))
@@ -321,6 +321,36 @@ def test_decompress_single_calls(gpu, test_files):
         assert res[0] == (len(data), data)
         assert res[1][0] == oracle_ref.decompress(f[:-1], len(data))[0]
         assert res[2][0] == -1
+
+
+@pytest.mark.parametrize("kind", ["fio", "mixed", "random"])
+def test_decompress_small_blocks_in_lds(gpu, kind):
+    """Blocks of <= 4608 bytes decoded with the whole output in LDS (auto
+    mode picks this form when every capacity is that small): exact and
+    +32 capacities, truncations and short capacities, values and bytes equal
+    the oracle's."""
+    rng = np.random.default_rng(4608 + len(kind))
+    data = _corpus(kind, 1 << 21, 91)
+    frames, caps, want = [], [], []
+    for i in range(3000):
+        n = int(rng.choice([4096, 4096, int(rng.integers(1, 4609))]))
+        s0 = int(rng.integers(0, data.size - n))
+        blk = data[s0:s0 + n].tobytes()
+        f = oracle_ref.compress(blk, BYU16)[1]
+        cap = n + (32 if i % 4 == 1 else 0)
+        if i % 9 == 2:
+            f = f[:int(rng.integers(1, len(f)))]
+        elif i % 9 == 5:
+            cap = max(0, n - int(rng.integers(1, 40)))
+        frames.append(f)
+        caps.append(cap)
+        want.append(oracle_ref.decompress(f, cap))
+    for mode in (DEC_AUTO, DEC_SMALL):
+        r, outs = _gpu_decompress(gpu, frames, caps, max_cap=max(caps), mode=mode)
+        for i, (er, eb) in enumerate(want):
+            assert r[i] == er, (mode, i, r[i], er)
+            if er >= 0:
+                assert outs[i] == eb, (mode, i)
 
 
 # ---------------------------------------------------------------------------
@@ -741,10 +771,12 @@ def test_decompress_pipelined_vs_wave_decoder(gpu, kind):
     r_wv, o_wv = _gpu_decompress(gpu, frames, caps, mode=DEC_WAVE)
     r_ck, o_ck = _gpu_decompress(gpu, frames, caps, mode=DEC_CHUNK)
     r_rl, o_rl = _gpu_decompress(gpu, frames, caps, mode=DEC_RELAY)
+    r_sm, o_sm = _gpu_decompress(gpu, frames, caps, mode=DEC_SMALL)
     for i, (er, eb) in enumerate(want):
-        assert r_wg[i] == er == r_wv[i] == r_ck[i] == r_rl[i], (i, r_wg[i], er, r_wv[i], r_ck[i], r_rl[i])
+        assert r_wg[i] == er == r_wv[i] == r_ck[i] == r_rl[i] == r_sm[i], \
+            (i, r_wg[i], er, r_wv[i], r_ck[i], r_rl[i], r_sm[i])
         if er >= 0:
-            assert o_wg[i] == eb == o_wv[i] == o_ck[i] == o_rl[i], i
+            assert o_wg[i] == eb == o_wv[i] == o_ck[i] == o_rl[i] == o_sm[i], i
 
 
 # ---------------------------------------------------------------------------

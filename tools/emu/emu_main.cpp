@@ -7,6 +7,8 @@
 //            one wave)
 //   emu_main -r FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (relay decoder,
 //            2 waves: parser + sequence copier)
+//   emu_main -l FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (one-wave decoder,
+//            LDS output for blocks of <= 4608 bytes without a dictionary)
 // compresses one block through the unmodified kernel source, prints the
 // return value and the iterator post-state words, and writes the frame.
 // With DICT_FILE the block is compressed in dictionary mode against the
@@ -61,8 +63,9 @@ static int decode_main(int argc, char** argv) {
     // the decoder reads the input window by aligned dwords (the GPU's word
     // granularity: the dword holding the last byte); the heap block covers it
     frame.reserve((frame.size() + 3) & ~(size_t)3);
-    // kDecPipe / kDecChunk / kDecRelay / kDecWave
-    const uint32_t mode = argv[1][1] == 'p' ? 2u : (argv[1][1] == 'c' ? 4u : (argv[1][1] == 'r' ? 5u : 1u));
+    // kDecPipe / kDecChunk / kDecRelay / kDecSmall / kDecWave
+    const char m = argv[1][1];
+    const uint32_t mode = m == 'p' ? 2u : (m == 'c' ? 4u : (m == 'r' ? 5u : (m == 'l' ? 6u : 1u)));
     emu_decompress_batch_mode(frame.data(), &so, &csize, out.data(), &doff, &cap, &ret, 1, &D, mode);
     char err[256];
     const int good = emu_decode_results(&ret, 1, err, sizeof err);
@@ -78,7 +81,8 @@ static int decode_main(int argc, char** argv) {
 
 int main(int argc, char** argv) {
     if (argc > 3 && argv[1][0] == '-' &&
-        (argv[1][1] == 'd' || argv[1][1] == 'p' || argv[1][1] == 'c' || argv[1][1] == 'r'))
+        (argv[1][1] == 'd' || argv[1][1] == 'p' || argv[1][1] == 'c' || argv[1][1] == 'r' ||
+         argv[1][1] == 'l'))
         return decode_main(argc, argv);
     if (argc < 3) {
         fprintf(stderr, "usage: emu_main BLOCK_FILE TABLE_CLASS [FRAME_OUT]\n");

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-4 check session: smoke, every -m gpu test, the default bench, then the
-# drop-in single calls under each path (direct host-mapped with the chunked /
+# drop-in single calls under each path (round-4 A/B: direct host-mapped with the chunked /
 # one-wave decoder, and the staged path).
 tag=${1:-r04}
 out=gpurun_out/$tag
