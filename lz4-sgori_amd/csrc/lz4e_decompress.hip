@@ -58,6 +58,12 @@ constexpr uint32_t kSink = 4 * kWave;               // a dword per lane for unwa
 constexpr uint32_t kSpan = 64 * 32 + 16 + 48;       // a fast batch's output, 16-B aligned start
 constexpr uint32_t kJump = 2 * kSpan;               // u16 per span byte (chain resolution)
 constexpr uint16_t kFinal = 0xFFFF;                 // jump entry of a byte whose value is final
+// Small blocks (decode_block's LDS form): output and input both staged in
+// LDS, at most kSmallOut bytes each, kSmallBuf bytes of LDS each.
+constexpr int32_t kSmallOut = 4608;  // 4 KiB blocks and their 4 KiB + 32 capacities
+constexpr uint32_t kSmallBuf = kSmallOut + 64;
+constexpr int32_t kSmallBatchOut = 1024;                  // fast-batch output cap there
+constexpr uint32_t kSmallJump = 2 * (kSmallBatchOut + 64);  // its jump table
 
 // LDS access types.  Every wider type may alias every other (may_alias):
 // the decoders read LDS bytes through whichever width suits the step, so no
@@ -86,12 +92,18 @@ struct InWindow {
     int32_t ring_lo; // lowest block position held by the ring
     uint32_t a, b, c;  // this lane's dword of A, B and C
     lu32* ring;      // kRing + kRingPad bytes of LDS
+    // Small blocks: the whole block staged in LDS (words 0..last, 64 bytes of
+    // slack after), read instead of HBM and instead of the ring; nullptr:
+    // HBM + ring.
+    const lu8* lb = nullptr;
 
     LZ4E_DEV uint32_t load(int32_t wi) const {
         wi = wi < 0 ? 0 : wi;
-        return w[wi < last ? wi : last];
+        wi = wi < last ? wi : last;
+        return lb ? ((const lu32*)lb)[wi] : w[wi];
     }
     LZ4E_DEV void put_ring(int32_t s, uint32_t v) const {
+        if (lb) return;
         const uint32_t slot = (uint32_t)s & 3;
         ring[slot * 64 + lane] = v;
         if (slot == 0 && lane < kRingPad / 4) ring[kRing / 4 + lane] = v;
@@ -169,15 +181,21 @@ struct InWindow {
     }
     // Little-endian 32 / 16 bits at block position p from the ring
     // (p in [ring_lo, base + 512 - 4 / 2)).
-    LZ4E_DEV uint32_t rd4(int32_t p) const {
-        return ld4(reinterpret_cast<const lu8*>(ring) + ((uint32_t)(p + shift) & (kRing - 1)));
+    LZ4E_DEV uint32_t rd4(int32_t p) const { return ld4(at(p)); }
+    // LDS address of block byte p (held: see holds); 16 bytes readable from it.
+    LZ4E_DEV const lu8* at(int32_t p) const {
+        if (lb) return lb + (uint32_t)(p + shift);
+        return reinterpret_cast<const lu8*>(ring) + ((uint32_t)(p + shift) & (kRing - 1));
     }
     LZ4E_DEV uint32_t rd16(int32_t p) const { return rd4(p) & 0xFFFFu; }
     // Block bytes [p, p + n) all held by the ring (at ring offsets that may
     // wrap: see wave_lit_ring).
-    LZ4E_DEV bool holds(int32_t p, int32_t n) const { return p >= ring_lo && p + n <= base + 512; }
+    LZ4E_DEV bool holds(int32_t p, int32_t n) const {
+        return lb || (p >= ring_lo && p + n <= base + 512);
+    }
     // The ring copy of block bytes [p, p + n), or nullptr when not all held.
     LZ4E_DEV const lu8* in_ring(int32_t p, int32_t n) const {
+        if (lb) return lb + (uint32_t)(p + shift);
         if (p < ring_lo || p + n > base + 512) return nullptr;
         const uint32_t i = (uint32_t)(p + shift) & (kRing - 1);
         // contiguous through the mirror, reads of up to 3 bytes past included
@@ -369,6 +387,10 @@ LZ4E_DEV void wave_match(uint8_t* out, int32_t op, uint32_t off, int32_t len, ui
     }
     // off < 1024: period P = off * ceil(1024 / off) >= 1024; the first P bytes
     // come from the final period [op-off, op), the rest from P bytes back.
+    // (Measured against 16-byte chunks built in registers from the period
+    // and against offset-doubling rounds: both slower on fio4k, 2.73 ->
+    // 3.15 / 4.91 ms one-wave: the byte loop's loads all read the final
+    // period and issue together.)
     const int32_t P = (int32_t)off * ((16 * kWave + off - 1) / off);
     const int32_t head = len < P ? len : P;
     for (int32_t t = lane; t < head; t += kWave) out[op + t] = out[src + (int32_t)(t % off)];
@@ -547,21 +569,50 @@ struct Parse {
     int32_t D;  // dictionary bytes before the output (<= 65536; 0: noDict)
     bool done;  // the final literal run has been parsed
 
+    // lin (small blocks, srcSize <= kSmallOut): stage the whole block into
+    // these kSmallBuf bytes of LDS first, one round trip for all its loads.
+    // (ip0, op0): resume at a sequence boundary (the lane decoder's hand-over)
     LZ4E_DEV void init(const uint8_t* in, int32_t srcSize, int32_t outSize, lu32* ring,
-                       uint32_t lane, int32_t dict = 0) {
+                       uint32_t lane, int32_t dict = 0, lu8* lin = nullptr, int32_t ip0 = 0,
+                       int32_t op0 = 0) {
         const uintptr_t a = reinterpret_cast<uintptr_t>(in);
         win.shift = (int32_t)(a & 3);
         win.w = (gcu32*)(a - win.shift);
         win.last = (srcSize + win.shift - 1) >> 2;
         win.lane = lane;
         win.ring = ring;
-        win.reload(0);
+        win.lb = nullptr;
+        if (lin) {
+            constexpr int kR = (kSmallOut + 4 + 16 * kWave - 1) / (16 * kWave);
+            uint32_t v[kR][4];
+#pragma unroll
+            for (int r = 0; r < kR; ++r)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int32_t wi = 4 * ((int32_t)lane + r * (int32_t)kWave) + q;
+                    v[r][q] = win.w[wi < win.last ? wi : win.last];
+                }
+#pragma unroll
+            for (int r = 0; r < kR; ++r) {
+                const int32_t wi = 4 * ((int32_t)lane + r * (int32_t)kWave);
+                if (wi <= win.last) {
+                    lu32* d = (lu32*)lin + wi;
+                    d[0] = v[r][0];
+                    d[1] = v[r][1];
+                    d[2] = v[r][2];
+                    d[3] = v[r][3];
+                }
+            }
+            lockstep();  // every lane reads the staged words next
+            win.lb = lin;
+        }
+        win.reload(ip0);
         iend = srcSize;
         oend = outSize;
         shortiend = iend - 14 - 2;  // :100-101
         shortoend = oend - 14 - 18; // :102-103
-        ip = 0;
-        op = 0;
+        ip = ip0;
+        op = op0;
         D = dict;
         done = false;
     }
@@ -580,13 +631,43 @@ enum ParseResult { kParsedFast, kParsedScalar, kParseFail };
 // The next batch of the token stream, with every bound check of the
 // reference in its order (lz4e_decompress.c:123-446).  kParsedFast: up to 64
 // sequences without extension bytes, far from both block ends (each literal
-// run <= 14, match length <= 18, output <= 32 bytes per sequence);
+// run <= 14, match length <= 18, output <= 32 bytes per sequence); with kExt
+// also sequences whose length fields carry one extension byte below
+// kExtByteMax (literal run <= 46, match <= 50 bytes), further from the ends;
 // kParsedScalar: one sequence of any length; kParseFail: malformed input or
 // too small a capacity, the return value is -(P.ip) - 1.  A fast batch's
 // output is at most cap_out (>= 32) bytes.
 struct NoLap {
     LZ4E_DEV void operator()(int) const {}
 };
+constexpr uint32_t kExtByteMax = 32;  // fast literal runs <= 46, matches <= 50 bytes
+// LZ4E_FAST_EXT=0 builds the decoders without extension sequences on the
+// fast path (A/B experiments).
+#ifndef LZ4E_FAST_EXT
+#define LZ4E_FAST_EXT 0
+#endif
+constexpr bool kFastExt = LZ4E_FAST_EXT;
+
+// Window offset (from ip) of the token after the one at offset p, for the
+// fast path: token t, e1 the byte after it; 255 when the sequence cannot be
+// on the fast path (without kExt: any extension byte; with kExt: a 255
+// extension byte, or one of kExtByteMax and more).  A match-length
+// extension byte is read from the ring (offsets past the window read stale
+// ring bytes: the result then exceeds 254 and is declined by the caller).
+template <bool kExt>
+LZ4E_DEV uint32_t fast_next(uint32_t t, uint32_t e1, uint32_t p, const InWindow& win, int32_t ip) {
+    const uint32_t Lt = t >> 4, Mt = t & 15;
+    if constexpr (!kExt) {
+        return (Lt != 15 && Mt != 15) ? p + Lt + 3 : 255u;
+    } else {
+        if (Lt == 15 && e1 >= kExtByteMax) return 255u;
+        const uint32_t q = Lt == 15 ? p + 2 + 15 + e1 : p + 1 + Lt;  // the offset's position
+        if (Mt != 15) return q + 2;
+        if (q + 2 > 253) return 255u;
+        const uint32_t e2 = win.rd4(ip + (int32_t)(q + 2)) & 0xFFu;
+        return e2 < kExtByteMax ? q + 3 : 255u;
+    }
+}
 // kVecExt: length-extension runs by 256-byte vector scans (the pipelined
 // decoder; the one-wave decoder keeps the byte loop: 2 more VGPRs would cost
 // it a wave per SIMD, and its <= 16 KiB blocks hold short runs).
@@ -597,7 +678,7 @@ struct NoLap {
 #define LZ4E_ONEWAVE_VEC_EXT false
 #endif
 constexpr bool kOneWaveVecExt = LZ4E_ONEWAVE_VEC_EXT;
-template <bool kVecExt = false, class Lap = NoLap>
+template <bool kVecExt = false, bool kExt = false, class Lap = NoLap>
 LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_out = 64 * 32,
                                  Lap lap = Lap()) {
     const int32_t iend = P.iend, oend = P.oend;
@@ -617,11 +698,11 @@ LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_
     if (fast) {
         win.follow(ip);
         wv = win.rd4(ip + 4 * (int32_t)lane);
-        // A batch that starts at a token with extension bytes -- every such
-        // token ends the fast batch before it -- is the scalar path's: lane
-        // 0's token would fail `cand` below, so no tables are composed.
-        const uint32_t t0 = lane_val(wv, 0) & 0xFFu;
-        fast = (t0 >> 4) != 15 && (t0 & 15) != 15;
+        // A batch that starts at a token the fast path cannot take -- every
+        // such token ends the fast batch before it -- is the scalar path's:
+        // lane 0's token would fail `cand` below, so no tables are composed.
+        const uint32_t w0 = lane_val(wv, 0);
+        fast = fast_next<kExt>(w0 & 0xFFu, (w0 >> 8) & 0xFFu, 0, win, ip) <= 254;
     }
     if (fast) {
         const int32_t r0 = ip - win.base;                  // < 256
@@ -630,11 +711,16 @@ LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_
         uint32_t J[6];
         {
             uint32_t j1 = 0;
+            const uint32_t wn = kExt ? shfl(wv, lane + 1) : 0u;  // byte 0: the byte after q = 3
 #pragma unroll
             for (uint32_t q = 0; q < 4; ++q) {
                 const uint32_t t = (wv >> (8 * q)) & 0xFFu, p = 4 * lane + q;
-                const uint32_t n = p + (t >> 4) + 3;
-                const bool go = (t >> 4) != 15 && (t & 15) != 15 && (int32_t)p <= jlim && n <= 254;
+                const uint32_t e1 = q < 3 ? (wv >> (8 * q + 8)) & 0xFFu : wn & 0xFFu;
+                const uint32_t n = fast_next<kExt>(t, e1, p, win, ip);
+                // an extension sequence also ends before jlim (its bytes stay
+                // in the window; the end checks of the general path hold)
+                const bool ext = kExt && ((t >> 4) == 15 || (t & 15) == 15);
+                const bool go = (int32_t)p <= jlim && n <= 254 && (!ext || (int32_t)n <= jlim);
                 j1 |= (go ? n : 255u) << (8 * q);
             }
             J[0] = j1;
@@ -651,11 +737,32 @@ LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_
         }
         lap(2);
         const uint32_t t = table_at(wv, x);  // token byte
-        const int32_t L = (int32_t)(t >> 4), Mt = (int32_t)(t & 15);
-        const bool cand = x != 255 && L != 15 && Mt != 15 && (int32_t)x <= jlim;
-        const int32_t lp = ip + (int32_t)x + 1;  // literal start
-        const int32_t off = cand ? (int32_t)win.rd16(lp + L) : 0;
-        const int32_t size = cand ? L + Mt + 4 : 0;
+        const int32_t Lt = (int32_t)(t >> 4), Mt = (int32_t)(t & 15);
+        int32_t L = Lt, M = Mt + 4, lp = ip + (int32_t)x + 1;  // literal start
+        bool cand, ext = false;
+        int32_t off, nxt;
+        if constexpr (kExt) {
+            // one extension byte per field at most (fast_next's rule)
+            const uint32_t e1 = table_at(wv, x + 1);  // (x <= 251 when cand)
+            if (Lt == 15) {
+                L = 15 + (int32_t)e1;
+                lp++;
+            }
+            const uint32_t ow = win.rd4(lp + L);  // offset, then the match extension byte
+            off = (int32_t)(ow & 0xFFFFu);
+            const uint32_t e2 = (ow >> 16) & 0xFFu;
+            if (Mt == 15) M = 19 + (int32_t)e2;
+            nxt = lp + L + 2 + (Mt == 15 ? 1 : 0);
+            ext = Lt == 15 || Mt == 15;
+            cand = x != 255 && (int32_t)x <= jlim && (Lt != 15 || e1 < kExtByteMax) &&
+                   (Mt != 15 || e2 < kExtByteMax) && (!ext || nxt - ip <= jlim);
+            off = cand ? off : 0;
+        } else {
+            cand = x != 255 && Lt != 15 && Mt != 15 && (int32_t)x <= jlim;
+            off = cand ? (int32_t)win.rd16(lp + L) : 0;
+            nxt = lp + L + 2;
+        }
+        const int32_t size = cand ? L + M : 0;
         const int32_t incl = (int32_t)wave_incl_add((uint32_t)size);
         const int32_t o_k = op + incl - size;
         const int32_t m_k = o_k + L;
@@ -663,10 +770,13 @@ LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_
         // input side guaranteed by jlim), match inside the block (:299-302),
         // and for offsets < 8 the _copy_match end check (:422-431); a source
         // in the dictionary takes _copy_match: offset inside dictionary +
-        // block (:299-302), then the extDict end check (:341-346)
+        // block (:299-302), then the extDict end check (:341-346).  An
+        // extension sequence takes the general path (:194-336): its output
+        // ending 32 bytes before oend passes every end check there.
         const bool ok = cand && o_k <= oend - 32 && incl <= cap_out &&
-                        (m_k >= off ? (off >= 8 || m_k + Mt + 4 <= oend - 5)
-                                    : (m_k - off + P.D >= 0 && m_k + Mt + 4 <= oend - 5));
+                        (!ext || o_k + size <= oend - 32) &&
+                        (m_k >= off ? (off >= 8 || m_k + M <= oend - 5)
+                                    : (m_k - off + P.D >= 0 && m_k + M <= oend - 5));
         const uint64_t okm = ballot(ok);
         const uint32_t nf = (~okm) ? ctz64(~okm) : kWave;  // first failing lane
         if (nf > 0) {
@@ -674,10 +784,10 @@ LZ4E_DEV ParseResult parse_batch(Parse& P, Batch& b, uint32_t lane, int32_t cap_
             b.L = L;
             b.op = o_k;
             b.off = off;
-            b.M = Mt + 4;
+            b.M = M;
             b.n = nf;
             P.op = op + lane_val((uint32_t)incl, nf - 1);
-            P.ip = lane_val((uint32_t)(lp + L + 2), nf - 1);  // the token after the last one
+            P.ip = lane_val((uint32_t)nxt, nf - 1);  // the token after the last one
             lap(3);
             return kParsedFast;
         }
@@ -823,6 +933,256 @@ LZ4E_DEV void copy_scalar_hbm(const Batch& b, const uint8_t* in, int32_t srcSize
     wave_fence();
 }
 
+// ---------------------------------------------------------------- lane-per-block decoder
+// Large batches of small blocks whose sequences are long (fio-style 4 KiB
+// buffers: ~14 sequences of ~300 bytes) leave the one-wave decoder parsing
+// one scalar sequence at a time with the other 63 lanes idle: ~24 k issue
+// cycles per block (tools/wavestamps.py).  Here every lane decodes a block of
+// its own: the reference's scalar loop (lz4e_decompress.c:123-446, the same
+// checks in the same order as parse_batch's exact path, so values and error
+// codes are the reference's), with 16-byte loads and stores per lane.  A
+// wave then costs about what one of its blocks costs, and a batch of
+// hundreds of thousands of blocks is resident at once.
+
+typedef __attribute__((address_space(1))) const uint8_t gcu8;
+LZ4E_DEV uint32_t ldb(const uint8_t* p, int32_t i) { return ((gcu8*)p)[i]; }
+// Global-address-space stores of the lane decoder (flat ones would also
+// count on lgkmcnt and make every wait a wait for both counters).
+typedef __attribute__((address_space(1))) uint64_t gu64w;
+typedef __attribute__((address_space(1))) uint16_t gu16w;
+LZ4E_DEV void gst_tail(uint8_t* p, uint4 c, uint32_t n) {
+    uint64_t lo = ((uint64_t)c.y << 32) | c.x, hi = ((uint64_t)c.w << 32) | c.z;
+    if (n & 8) {
+        *(gu32w*)p = (uint32_t)lo;
+        *(gu32w*)(p + 4) = (uint32_t)(lo >> 32);
+        p += 8;
+        lo = hi;
+        hi = 0;
+    }
+    if (n & 4) {
+        *(gu32w*)p = (uint32_t)lo;
+        p += 4;
+        lo = (lo >> 32) | (hi << 32);
+    }
+    if (n & 2) {
+        *(gu16w*)p = (uint16_t)lo;
+        p += 2;
+        lo >>= 16;
+    }
+    if (n & 1) *(gu8*)p = (uint8_t)lo;
+}
+
+// Per-lane copy of len (1..256) bytes, src + len <= dst or another buffer:
+// every load issued before the first store (one round trip per 256 bytes;
+// the lane decoder runs few waves per CU, so registers are plentiful).
+// Loads never read at or past lim.
+LZ4E_DEV void lane_copy256(uint8_t* dst, const uint8_t* src, int32_t len, const uint8_t* lim) {
+    const uint32_t nch = ((uint32_t)len + 15) >> 4;
+    if (src + 16 * nch > lim) {
+        for (int32_t t = 0; t < len; ++t) *(gu8*)(dst + t) = (uint8_t)ldb(src, t);
+        return;
+    }
+    uint4 c[16];
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) c[i] = i < nch ? ldg16(src + 16 * i) : make_uint4(0, 0, 0, 0);
+    const uint32_t full = (uint32_t)len >> 4, tail = (uint32_t)len & 15;
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) {
+        if (i < full) stg16(dst + 16 * i, c[i]);
+        else if (i == full && tail) gst_tail(dst + 16 * i, c[i], tail);
+    }
+}
+
+// Per-lane copy of len bytes, src + len <= dst or another buffer.
+LZ4E_DEV void lane_copy_any(uint8_t* dst, const uint8_t* src, int32_t len, const uint8_t* lim) {
+    for (int32_t t = 0; t < len; t += 256) lane_copy256(dst + t, src + t, len - t < 256 ? len - t : 256, lim);
+}
+
+// Per-lane match copy out[t] = out[t - off] for t in [0, len), any overlap
+// (offset 0: zeros).  Periods below 16 are first widened from registers
+// (the final period, then whole multiples of it up to >= 16 bytes); then
+// piece [t, t + c) comes from D bytes back, D a multiple of off with
+// c <= D <= t (doubling), so every source byte is written before its piece.
+LZ4E_DEV void lane_match_any(uint8_t* dst, uint32_t off, int32_t len, const uint8_t* lim) {
+    int32_t t = 0;
+    if (off == 0) {
+        for (; t + 16 <= len; t += 16) stg16(dst + t, make_uint4(0, 0, 0, 0));
+        if (t < len) gst_tail(dst + t, make_uint4(0, 0, 0, 0), (uint32_t)(len - t));
+        return;
+    }
+    uint32_t D = off;
+    if (off < 16) {
+        const uint32_t H = off * ((15 + off) / off);  // >= 16, a multiple of off
+        const int32_t h = len < (int32_t)H ? len : (int32_t)H;
+        if (dst - off + 16 > lim) {
+            for (; t < h; ++t) *(gu8*)(dst + t) = (uint8_t)ldb(dst, t - (int32_t)off);
+        } else {
+            const uint4 p = ldg16(dst - off);
+            uint32_t j = 0;
+            for (; t < h; ++t) {
+                *(gu8*)(dst + t) = (uint8_t)pat_byte(p, j);
+                j = (j + 1 == off) ? 0 : j + 1;
+            }
+        }
+        D = H;
+    }
+    while (t < len) {
+        int32_t c = len - t < (int32_t)D ? len - t : (int32_t)D;
+        c = c < 256 ? c : 256;
+        lane_copy256(dst + t, dst + t - D, c, lim);
+        t += c;
+        while (2 * D <= (uint32_t)t) D *= 2;
+    }
+}
+
+// A lane's 16-byte window of its input (token, extension and offset bytes
+// mostly come from one load): bytes [base, base + 16) in w.
+struct LaneIn {
+    const uint8_t* in;
+    int32_t n, base;
+    uint4 w;
+    LZ4E_DEV void fill(int32_t p) {
+        base = p;
+        if (p + 16 <= n) {
+            w = ldg16(in + p);
+        } else {
+            uint32_t x[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int32_t k = 0; k < 16; ++k)
+                if (p + k < n) x[k >> 2] |= ldb(in, p + k) << (8 * (k & 3));
+            w = make_uint4(x[0], x[1], x[2], x[3]);
+        }
+    }
+    // byte p (< n)
+    LZ4E_DEV uint32_t byte(int32_t p) {
+        if ((uint32_t)(p - base) >= 16) fill(p);
+        return pat_byte(w, (uint32_t)(p - base));
+    }
+};
+
+// One block on one lane: the return value of LZ4E_decompress_safe (D
+// dictionary bytes before out).
+// A lane whose block turns out to hold short sequences (fewer than
+// kLaneBailBytes output bytes per sequence over the last kLaneBailSeqs
+// sequences: text, tables) hands the block over at a sequence
+// boundary -- one lane left decoding such a block would hold the whole
+// launch for milliseconds: it
+// returns kLaneHandOver with (*ip_out, *op_out), and the one-wave decoder
+// resumes there (a lane pays a few round trips per sequence, which only
+// long sequences amortise).
+constexpr int32_t kLaneHandOver = INT32_MIN;
+#ifndef LZ4E_LANE_BAIL_SEQS
+#define LZ4E_LANE_BAIL_SEQS 4
+#endif
+#ifndef LZ4E_LANE_FIRST_LIT
+#define LZ4E_LANE_FIRST_LIT 200
+#endif
+constexpr int32_t kLaneBailSeqs = LZ4E_LANE_BAIL_SEQS;
+constexpr int32_t kLaneBailBytes = 64;
+constexpr uint32_t kLaneFirstLit = LZ4E_LANE_FIRST_LIT;  // (fio-style: 256)
+LZ4E_DEV int32_t lane_decode(const uint8_t* in, int32_t srcSize, uint8_t* out, int32_t outSize,
+                             int32_t D, bool may_bail, int32_t* ip_out, int32_t* op_out) {
+    const int32_t iend = srcSize, oend = outSize;
+    const int32_t shortiend = iend - 14 - 2, shortoend = oend - 14 - 18;  // :100-103
+    const uint8_t* ilim = in + srcSize;
+    const uint8_t* olim = out + outSize;
+    int32_t ip = 0, op = 0;
+    LaneIn I;
+    I.in = in;
+    I.n = srcSize;
+    I.fill(0);
+    if (may_bail) {
+        // a block that opens with a short literal run is most likely one of
+        // short sequences: straight to the one-wave decoder
+        // (nor does one whose first match is short: both must be long)
+        const uint32_t t0 = I.byte(0);
+        const uint32_t l0 = (t0 >> 4) == 15 && srcSize > 1 ? 15 + I.byte(1) : t0 >> 4;
+        const int32_t q = 2 + (int32_t)l0 + 2;  // the first match's extension byte
+        const bool long_m = l0 >= kLaneFirstLit && (t0 & 15) == 15 && q < srcSize && I.byte(q) >= 64 - 19;
+        if (!long_m) {
+            *ip_out = 0;
+            *op_out = 0;
+            return kLaneHandOver;
+        }
+    }
+    int32_t op_chk = 0;  // output position at the last check
+    for (int32_t nseq = 0;; ++nseq) {
+        if (may_bail && nseq >= kLaneBailSeqs && nseq % kLaneBailSeqs == 0) {
+            if (op - op_chk >= kLaneBailBytes * kLaneBailSeqs) {
+                op_chk = op;
+                goto go_on;
+            }
+            *ip_out = ip;
+            *op_out = op;
+            return kLaneHandOver;
+        }
+    go_on:
+        const uint32_t token = I.byte(ip);
+        ip++;
+        uint32_t length = token >> 4;  // saturates at kSat
+        int32_t offset;
+        if (length != 15 && ip < shortiend && op <= shortoend) {
+            // two-stage shortcut (:150-191)
+            if (length) lane_copy256(out + op, in + ip, (int32_t)length, ilim);
+            op += (int32_t)length;
+            ip += (int32_t)length;
+            offset = (int32_t)(I.byte(ip) | (I.byte(ip + 1) << 8));
+            ip += 2;
+            length = token & 15;
+            if (length != 15 && offset >= 8 && op >= offset) {
+                lane_match_any(out + op, (uint32_t)offset, (int32_t)length + 4, olim);
+                op += (int32_t)length + 4;
+                continue;
+            }
+        } else {
+            if (length == 15) {  // :194-220
+                if (ip >= iend - 15) break;
+                uint32_t s;
+                do {
+                    s = I.byte(ip);
+                    ip++;
+                    length = length + s > kSat ? kSat : length + s;
+                } while (ip < iend - 15 && s == 255);
+            }
+            const uint32_t cpy = (uint32_t)op + length;  // :223-288
+            const uint32_t iln = (uint32_t)ip + length;
+            if (ugt(cpy, oend - 12) || ugt(iln, iend - 8)) {
+                if (iln != (uint32_t)iend || ugt(cpy, oend)) break;
+                lane_copy_any(out + op, in + ip, (int32_t)length, ilim);  // final literal run
+                return (int32_t)cpy;
+            }
+            // the window after the literal run loads under the run's copy
+            if ((uint32_t)(ip + (int32_t)length - I.base) + 2 > 16) I.fill(ip + (int32_t)length);
+            lane_copy_any(out + op, in + ip, (int32_t)length, ilim);
+            ip += (int32_t)length;
+            op = (int32_t)cpy;
+            offset = (int32_t)(I.byte(ip) | (I.byte(ip + 1) << 8));  // :291-296
+            ip += 2;
+            length = token & 15;
+        }
+        // _copy_match (:298-336, :422-431)
+        if (op - offset + D < 0) break;
+        if (length == 15) {
+            uint32_t s;
+            bool bad = false;
+            do {
+                s = I.byte(ip);
+                ip++;
+                if (ip > iend - 5) {
+                    bad = true;
+                    break;
+                }
+                length = length + s > kSat ? kSat : length + s;
+            } while (s == 255);
+            if (bad) break;
+        }
+        if (ugt((uint32_t)op + length + 4, oend - 5)) break;
+        lane_match_any(out + op, (uint32_t)offset, (int32_t)length + 4, olim);
+        op += (int32_t)length + 4;
+    }
+    return -ip - 1;
+}
+
 // ---------------------------------------------------------------- small blocks in LDS
 // A block of at most kSmallOut output bytes without a dictionary (4 KiB
 // blocks, the drop-in single calls) can keep its whole output in LDS: a
@@ -830,18 +1190,14 @@ LZ4E_DEV void copy_scalar_hbm(const Batch& b, const uint8_t* in, int32_t srcSize
 // data) then copies LDS to LDS at LDS latency instead of a store, a load
 // that waits behind it and another store in HBM per sequence, and the block
 // leaves in one pass of 16-byte stores at the end.
-constexpr int32_t kSmallOut = 4608;  // 4 KiB blocks and their 4 KiB + 32 capacities
-constexpr uint32_t kSmallBuf = kSmallOut + 64;
 
 // Whole-wave copy of n (<= 1024 per call of a round) bytes of a literal run
 // from the input ring (block bytes [p, p + n) held by it): 16 bytes per lane,
 // ring offsets wrap through the mirror.
 LZ4E_DEV void wave_lit_ring(lu8* dst, const InWindow& w, int32_t p, int32_t n, lu8* sink,
                             uint32_t lane) {
-    const lu8* r = reinterpret_cast<const lu8*>(w.ring);
     for (int32_t k = 16 * (int32_t)lane; k < n; k += 16 * (int32_t)kWave)
-        piece16(dst + k, r + ((uint32_t)(p + w.shift + k) & (kRing - 1)),
-                (uint32_t)(n - k < 16 ? n - k : 16), sink);
+        piece16(dst + k, w.at(p + k), (uint32_t)(n - k < 16 ? n - k : 16), sink);
 }
 
 // Whole-wave copy of n (<= kSmallOut) literal bytes from HBM into LDS: every
@@ -879,6 +1235,26 @@ LZ4E_DEV void wave_match_lds(lu8* out, int32_t op, uint32_t off, int32_t len, lu
             put16(out + op + k, make_uint4(0, 0, 0, 0), (uint32_t)(len - k < 16 ? len - k : 16), sink);
         return;
     }
+    if (off < 16) {
+        // short periods from registers (see wave_match): one LDS read of the
+        // final period, then every chunk without waiting on earlier ones
+        const lu8* pp = out + op - (int32_t)off;
+        const uint4 pv = make_uint4(ld4(pp), ld4(pp + 4), ld4(pp + 8), ld4(pp + 12));
+        const uint32_t step = (16u * kWave) % off;
+        uint32_t ph = (16u * lane) % off;
+        for (int32_t k = 16 * (int32_t)lane; k < len; k += 16 * (int32_t)kWave) {
+            uint32_t w[4] = {0, 0, 0, 0}, j = ph;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                w[q >> 2] |= pat_byte(pv, j) << (8 * (q & 3));
+                j = j + 1 == off ? 0 : j + 1;
+            }
+            put16(out + op + k, make_uint4(w[0], w[1], w[2], w[3]), (uint32_t)(len - k < 16 ? len - k : 16), sink);
+            ph += step;
+            ph = ph >= off ? ph - off : ph;
+        }
+        return;
+    }
     int32_t t = 0, D = (int32_t)off;
     while (t < len) {
         int32_t c = len - t < D ? len - t : D;
@@ -901,7 +1277,8 @@ LZ4E_DEV void copy_scalar_lds(const Batch& b, const InWindow& win, const uint8_t
     const int32_t ls = lane_val((uint32_t)b.ls, 0);
     const int32_t M = lane_val((uint32_t)b.M, 0), off = lane_val((uint32_t)b.off, 0);
     if (L > 0) {
-        if (win.holds(ls, L) && L <= 16 * (int32_t)kWave) wave_lit_ring(obuf + op, win, ls, L, sink, lane);
+        if (win.holds(ls, L) && (win.lb || L <= 16 * (int32_t)kWave))
+            wave_lit_ring(obuf + op, win, ls, L, sink, lane);
         else wave_lit_hbm(obuf + op, in, ls, L, srcSize, sink, lane);
         lockstep();
     }
@@ -931,7 +1308,8 @@ struct Stamps {
 template <bool kStamps, bool kLdsOut = false>
 LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, int32_t outSize,
                            int32_t* ret_slot, uint64_t* dbg, uint32_t lane, lu8* span_buf,
-                           lu32* ring, lu16* jump, int32_t dict, lu8* obuf = nullptr) {
+                           lu32* ring, lu16* jump, int32_t dict, lu8* sinkb, lu8* obuf = nullptr,
+                           lu8* lin = nullptr, int32_t ip0 = 0, int32_t op0 = 0) {
     Stamps st;
     auto lap = [&](int ph) {
         if constexpr (kStamps) {
@@ -941,13 +1319,14 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
         }
     };
     if constexpr (kStamps) st.t = clock64();
-    lu8* sink = (lu8*)ring + kRing + kRingPad + 4 * lane;  // (span follows the sink)
+    lu8* sink = sinkb + 4 * lane;
     Parse P;
-    P.init(in, srcSize, outSize, ring, lane, dict);
+    P.init(in, srcSize, outSize, ring, lane, dict, lin, ip0, op0);
 
     for (;;) {
         Batch b;
-        const ParseResult pr = parse_batch<kOneWaveVecExt>(P, b, lane);
+        const ParseResult pr =
+            parse_batch<kOneWaveVecExt, kFastExt>(P, b, lane, kLdsOut ? kSmallBatchOut : 64 * 32);
         if (pr == kParseFail) {
             if (lane == 0) *ret_slot = -P.ip - 1;
             break;
@@ -985,7 +1364,11 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
                 if (n0 > 0) lane_copy(span + (ms - a0), obuf + ss, n0, sink);
             } else if (n0 > 0) {
                 put16(span + (ms - a0), h0, n0 < 16 ? n0 : 16, sink);
-                if (n0 > 16) put16(span + (ms - a0) + 16, h1, n0 - 16, sink);
+                if (n0 > 16) put16(span + (ms - a0) + 16, h1, n0 < 32 ? n0 - 16 : 16, sink);
+                // extension matches (up to 50 bytes): the rest in a
+                // second round trip, rare
+                for (int32_t t = 32; t < n0; t += 16)
+                    put16(span + (ms - a0) + t, ldg16(gout + ss + t), n0 - t < 16 ? n0 - t : 16, sink);
             }
             lap(1);
             const int32_t ms2 = ms + n0, m2 = b.M - n0, me = ms + b.M;
@@ -1110,17 +1493,99 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
     uint8_t* out = dst + dst_off[b];
     uint64_t* d = kStamps && dbg ? dbg + 8 * (size_t)b : nullptr;
     if (special_case(in, srcSize, outSize, ret + b, lane)) return;
-    // LDS: [input ring + mirror] [store sink] [span | small-block output] [jump table]
-    constexpr uint32_t kMid = kSmall ? kSmallBuf : kSpan;
-    __shared__ __attribute__((aligned(16))) uint8_t smem[kRing + kRingPad + kSink + kMid + kJump];
-    lu8* mid = (lu8*)(smem + kRing + kRingPad + kSink);
-    lu16* jump = (lu16*)(smem + kRing + kRingPad + kSink + kMid);
+    // LDS: [input ring + mirror] [store sink] [span] [jump table]; small
+    // blocks: [store sink] [output] [jump table] [input]
+    constexpr uint32_t kWaveLds = kRing + kRingPad + kSink + kSpan + kJump;
+    constexpr uint32_t kSmallLds = kSink + kSmallBuf + kSmallJump + kSmallBuf;
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kSmall && kSmallLds > kWaveLds ? kSmallLds : kWaveLds];
     const int32_t dict = dict_of(dict_len, b);
-    if (kSmall && dict == 0 && outSize <= kSmallOut)
-        decode_block<kStamps, true>(in, srcSize, out, outSize, ret + b, d, lane, mid, (lu32*)smem, jump,
-                                    0, mid);
-    else
-        decode_block<kStamps>(in, srcSize, out, outSize, ret + b, d, lane, mid, (lu32*)smem, jump, dict);
+    if (kSmall && dict == 0 && outSize <= kSmallOut && srcSize <= kSmallOut) {
+        lu8* obuf = (lu8*)(smem + kSink);
+        decode_block<kStamps, true>(in, srcSize, out, outSize, ret + b, d, lane, obuf, nullptr,
+                                    (lu16*)(obuf + kSmallBuf), 0, (lu8*)smem, obuf,
+                                    obuf + kSmallBuf + kSmallJump);
+    } else {
+        lu8* sinkb = (lu8*)(smem + kRing + kRingPad);
+        decode_block<kStamps>(in, srcSize, out, outSize, ret + b, d, lane, sinkb + kSink, (lu32*)smem,
+                              (lu16*)(sinkb + kSink + kSpan), dict, sinkb);
+    }
+}
+
+// The lane-per-block decoder (see lane_decode): block b on lane b % 256 of
+// workgroup b / 256.
+constexpr uint32_t kLaneWg = 256;
+#ifndef LZ4E_LANE_PAD
+#define LZ4E_LANE_PAD 0
+#endif
+__global__ __launch_bounds__(kLaneWg) void decompress_lane_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
+    const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
+    const int32_t* __restrict__ dict_len, uint32_t* __restrict__ handover, uint64_t* __restrict__ dbg) {
+#if LZ4E_LANE_PAD
+    // residency cap (experiments): LDS the workgroup never uses
+    __shared__ uint8_t pad[LZ4E_LANE_PAD];
+    if (nblocks == 0xFFFFFFFFu) ((volatile uint8_t*)pad)[threadIdx.x] = 1;
+#endif
+    const uint32_t b = blockIdx.x * kLaneWg + threadIdx.x, lane = lane_id();
+    // (no lane leaves early: the hand-over below is a whole-wave step)
+    bool act = b < nblocks;
+    int32_t r = 0, ip = 0, op = 0;
+    const uint64_t t0 = dbg ? clock64() : 0;
+    if (act) {
+        const int32_t srcSize = src_len[b], outSize = dst_cap[b];
+        const uint8_t* in = src + src_off[b];
+        if (special_case(in, srcSize, outSize, ret + b, 0)) act = false;
+        else r = lane_decode(in, srcSize, dst + dst_off[b], outSize, dict_of(dict_len, b), handover != nullptr, &ip, &op);
+    }
+    // hand-over list [count, (block, ip, op) ...] for decompress_resume_kernel:
+    // one atomic per wave (one per lane serialised 65 536 of them on one
+    // address: ~0.3 ms)
+    const bool ho = act && r == kLaneHandOver;
+    const uint64_t m = ballot(ho);
+    if (m) {
+        const uint32_t lead = ctz64(m);
+        uint32_t base = 0;
+        if (lane == lead) base = atomicAdd(handover, popc64(m));
+        base = shfl(base, lead);
+        if (ho) {
+            const uint32_t k = base + popc64(m & ((1ull << lane) - 1));
+            handover[1 + 3 * k] = b;
+            handover[2 + 3 * k] = (uint32_t)ip;
+            handover[3 + 3 * k] = (uint32_t)op;
+        }
+    }
+    if (act && !ho) ret[b] = r;
+    if (dbg && act) {  // stamped build: the lane's cycles, where it stopped, handed over
+        dbg[8 * (size_t)b + 6] = clock64() - t0;
+        dbg[8 * (size_t)b + 7] = ((uint64_t)(ho ? 1 : 0) << 63) | (uint32_t)op;
+    }
+}
+
+// The blocks the lane decoder handed over, one wave each from their
+// sequence boundary on (decode_block's HBM form; the output before it is in
+// HBM): workgroup i takes entry i, those past the count leave at once (as
+// balanced as the one-wave kernel itself; a fixed grid striding over the
+// list measured 1.31 vs 1.12 ms when every block was handed over).
+template <bool kStamps>
+__global__ __launch_bounds__(64) void decompress_resume_kernel(
+    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+    const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
+    const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, const uint32_t* __restrict__ handover,
+    uint64_t* __restrict__ dbg, const int32_t* __restrict__ dict_len) {
+    __shared__ __attribute__((aligned(16))) uint8_t smem[kRing + kRingPad + kSink + kSpan + kJump];
+    const uint32_t lane = lane_id();
+    const uint32_t cnt = handover[0];
+    for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {  // (one pass: grid = every block)
+        const uint32_t b = handover[1 + 3 * i];
+        const int32_t ip0 = (int32_t)handover[2 + 3 * i], op0 = (int32_t)handover[3 + 3 * i];
+        uint64_t* d = kStamps && dbg ? dbg + 8 * (size_t)b : nullptr;
+        lu8* sinkb = (lu8*)(smem + kRing + kRingPad);
+        decode_block<kStamps>(src + src_off[b], src_len[b], dst + dst_off[b], dst_cap[b], ret + b, d, lane,
+                              sinkb + kSink, (lu32*)smem, (lu16*)(sinkb + kSink + kSpan), dict_of(dict_len, b),
+                              sinkb, nullptr, nullptr, ip0, op0);
+        lockstep();  // the next block reuses the LDS
+    }
 }
 
 // ============================================================================
@@ -1340,14 +1805,26 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
     st.lap(kStamps, kStPtrs);
     // the loaded bytes into the span
     if (valid && b.L > 0) {
-        if (lfast) put16(span + (b.op - a0), lv, (uint32_t)b.L, sink);
-        else
+        if (lfast) {
+            put16(span + (b.op - a0), lv, b.L < 16 ? (uint32_t)b.L : 16u, sink);
+            // extension literal runs (up to 46 bytes, rare): the
+            // rest in a second round trip; ls + L <= srcSize - 18 on the
+            // fast path
+#pragma clang loop unroll(disable) vectorize(disable)
+            for (int32_t t = 16; t < b.L; t += 16)
+                put16(span + (b.op - a0) + t, ldg16(in + b.ls + t), (uint32_t)(b.L - t < 16 ? b.L - t : 16),
+                      sink);
+        } else {
 #pragma clang loop unroll(disable) vectorize(disable)
             for (int32_t t = 0; t < b.L; ++t) span[b.op - a0 + t] = in[b.ls + t];
+        }
     }
     if (nf > 0) {
         put16(span + (ms - a0), h0, nf < 16 ? nf : 16, sink);
-        if (nf > 16) put16(span + (ms - a0) + 16, h1, nf - 16, sink);
+        if (nf > 16) put16(span + (ms - a0) + 16, h1, nf < 32 ? nf - 16 : 16, sink);
+#pragma clang loop unroll(disable) vectorize(disable)
+        for (int32_t t = 32; t < nf; t += 16)  // extension matches: a second round trip
+            put16(span + (ms - a0) + t, ldg16(gout + ss + t), (uint32_t)(nf - t < 16 ? nf - t : 16), sink);
     }
     if (valid && b.off == 0)  // offset 0 writes zeros (:313, 407-415)
 #pragma clang loop unroll(disable) vectorize(disable)
@@ -1525,7 +2002,7 @@ __global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
         for (;;) {
             Batch bt;
             const int32_t lo = P.op;
-            const ParseResult pr = parse_batch<true>(P, bt, lane, kPipeOut, [&](int k) {
+            const ParseResult pr = parse_batch<true, kFastExt>(P, bt, lane, kPipeOut, [&](int k) {
                 if (kStamps) st.lap(true, kStPWin + k);
             });
             st.lap(kStamps, kStParse);
@@ -2689,6 +3166,13 @@ __global__ __launch_bounds__(2 * kWave) void decompress_relay_kernel(
 // profiles/r04/decmodes.txt); at 64 KiB the pipelined decoder's per-block
 // speed wins (silesia64k 0.85 vs 1.20 ms).
 constexpr uint32_t kPipeMinCap = 16384;
+// Batches of at least this many blocks of <= kSmallOut bytes take the lane
+// decoder (blocks that open with a short sequence go straight on to the
+// one-wave decoder): a lane's block takes ~1 ms, which only pays once the
+// one-wave decoder needs dozens of rounds of workgroups (fio4k, 262 144
+// blocks: 2.74 -> 1.53 ms; 4 KiB Silesia-proxy blocks, all handed over:
+// 1.13 -> 1.12 ms; tools/decmodes.py).
+constexpr uint32_t kLaneMinBlocks = 131072;
 constexpr uint32_t kPipeMaxCap = 131072;
 
 // Launch order of the pipelined decoder when the batch takes more than one
@@ -2719,10 +3203,11 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
                              : (env[0] == 'p' ? kDecPipe
                                               : (env[0] == 'c' ? kDecChunk : (env[0] == 'r' ? kDecRelay : kDecAuto)));
     if (mode == kDecAuto && env && env[0] == 's') mode = kDecSmall;
+    if (mode == kDecAuto && env && env[0] == 'l') mode = kDecLane;
     if (mode == kDecAuto)
         mode = (a.max_cap == 0 || (a.max_cap >= kPipeMinCap && a.max_cap < kPipeMaxCap))
                    ? kDecPipe
-                   : (a.max_cap <= (uint32_t)kSmallOut ? kDecSmall : kDecWave);
+                   : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks >= kLaneMinBlocks ? kDecLane : kDecWave);
     if (mode == kDecRelay) {
         const int om = launch_order_mode(false);
         uint32_t* order = nullptr;
@@ -2775,6 +3260,31 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
                            a.nblocks, dbg, a.dict_len, (const uint32_t*)order);
         const hipError_t err = hipGetLastError();
         if (order) (void)hipFreeAsync(order, stream);
+        return err;
+    }
+    if (mode == kDecLane) {
+        // hand-over list (count + 3 words per block); without it every lane
+        // decodes its block to the end
+        uint32_t* ho = nullptr;
+        if (hipMallocAsync((void**)&ho, 4 + 12 * (size_t)a.nblocks, stream) != hipSuccess ||
+            hipMemsetAsync(ho, 0, 4, stream) != hipSuccess) {
+            (void)hipGetLastError();
+            if (ho) (void)hipFreeAsync(ho, stream);
+            ho = nullptr;
+        }
+        hipLaunchKernelGGL(decompress_lane_kernel, dim3((a.nblocks + kLaneWg - 1) / kLaneWg), dim3(kLaneWg), 0,
+                           stream, a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
+                           a.dict_len, ho, dbg);
+        hipError_t err = hipGetLastError();
+        if (ho) {
+            if (err == hipSuccess) {
+                hipLaunchKernelGGL((decompress_resume_kernel<kStamps>), dim3(a.nblocks), dim3(kWave), 0, stream, a.src,
+                                   a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, ho, dbg,
+                                   a.dict_len);
+                err = hipGetLastError();
+            }
+            (void)hipFreeAsync(ho, stream);
+        }
         return err;
     }
     if (mode == kDecSmall)

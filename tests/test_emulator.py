@@ -210,6 +210,47 @@ def test_emulated_small_block_decoder_sanitized(emu_exe, tmp_path, kind, mode):
             assert got[1] == want[1], rep
 
 
+LANE_CASES = [(k, m) for k in ("text", "fio", "random", "head") for m in range(5)]
+
+
+@pytest.mark.parametrize("kind,mode", LANE_CASES, ids=[f"{k}-{m}" for k, m in LANE_CASES])
+def test_emulated_lane_decoder_sanitized(emu_exe, tmp_path, kind, mode):
+    """The lane-per-block decoder (one block per lane) and its hand-over to
+    the one-wave decoder: blocks that open with a short literal run go over
+    at once (text), long-sequence blocks stay on their lane (fio, random),
+    and "head" blocks (230 random bytes, 200 zeros, then text) go over
+    mid-block at a sequence boundary.  Valid frames (mode 0), truncations (1), bit
+    flips (2), short capacity (3) and a dictionary (4) equal the oracle."""
+    rng = np.random.default_rng(700 + mode)
+    for rep in range(3):
+        n = int(rng.choice([4096, int(rng.integers(13, 12000))]))
+        if kind == "fio":
+            data = corpus.fio_pattern(16 * 4096)[(rep + 2) * 4096 - 9000:][:n + 9000].tobytes()
+        elif kind == "head":
+            t = _block("text", n + 9000, 5 + rep).tobytes()
+            r = np.random.default_rng(rep).integers(0, 256, 230, dtype=np.uint8).tobytes() + bytes(200)
+            data = t[:9000] + (r + t[9000:])[:n]
+        else:
+            data = _block(kind, n + 9000, 21 + rep + n).tobytes()
+        dic, blk = (data[:9000], data[9000:]) if mode == 4 else (b"", data[9000:9000 + n] if kind == "head" else data[:n])
+        f = oracle_ref.compress_dict(blk, dic)[1] if mode == 4 else oracle_ref.compress(blk, BYU16)[1]
+        cap = len(blk)
+        if mode == 1:
+            f = f[:int(rng.integers(1, len(f)))]
+        elif mode == 2:
+            fb = bytearray(f)
+            for _ in range(3):
+                fb[int(rng.integers(0, len(fb)))] ^= 1 << int(rng.integers(0, 8))
+            f = bytes(fb)
+        elif mode == 3:
+            cap = max(0, len(blk) - int(rng.integers(1, 40)))
+        want = oracle_ref.decompress_dict(f, cap, dic)
+        got = _emu_decode(emu_exe, tmp_path, f, cap, dic, "-n")
+        assert got[0] == want[0], (rep, got[0], want[0])
+        if want[0] >= 0:
+            assert got[1] == want[1], rep
+
+
 VEC_CASES = [(k, m) for k in ("random", "runs", "text") for m in range(4)]
 
 

@@ -72,7 +72,7 @@ def _gpu_compress(amd, blocks, ttypes, caps=None):
     return r, frames, ax
 
 
-DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_CHUNK, DEC_RELAY, DEC_SMALL = 0, 1, 2, 4, 5, 6
+DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_CHUNK, DEC_RELAY, DEC_SMALL, DEC_LANE = 0, 1, 2, 4, 5, 6, 7
 
 
 def _gpu_decompress(amd, frames, caps, csizes=None, max_cap=None, mode=DEC_AUTO):
@@ -276,8 +276,8 @@ def test_decompress_batch_vs_oracle(gpu, kind):
         assert outs[i] == eo == expect[i]
 
 
-@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_CHUNK, DEC_RELAY, DEC_PIPE, DEC_WAVE, DEC_SMALL],
-                         ids=["auto", "chunk", "relay", "pipe", "wave", "small"])
+@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_CHUNK, DEC_RELAY, DEC_PIPE, DEC_WAVE, DEC_SMALL, DEC_LANE],
+                         ids=["auto", "chunk", "relay", "pipe", "wave", "small", "lane"])
 @pytest.mark.parametrize("mode", ["truncate", "flip", "garbage", "small_cap", "csize"])
 def test_decompress_error_codes(gpu, mode, dec):
     rng = np.random.default_rng(1234 + len(mode))
@@ -323,19 +323,24 @@ def test_decompress_single_calls(gpu, test_files):
         assert res[2][0] == -1
 
 
-@pytest.mark.parametrize("kind", ["fio", "mixed", "random"])
+@pytest.mark.parametrize("kind", ["fio", "mixed", "random", "head"])
 def test_decompress_small_blocks_in_lds(gpu, kind):
-    """Blocks of <= 4608 bytes decoded with the whole output in LDS (auto
-    mode picks this form when every capacity is that small): exact and
-    +32 capacities, truncations and short capacities, values and bytes equal
-    the oracle's."""
+    """Blocks of <= 4608 bytes: the one-wave decoder's LDS form (whole
+    output in LDS) and the lane-per-block decoder with its hand-over to the
+    one-wave decoder ("head": 230 random bytes and 200 zeros, then short
+    sequences),
+    and auto mode: exact and +32 capacities, truncations and short
+    capacities, values and bytes equal the oracle's."""
     rng = np.random.default_rng(4608 + len(kind))
-    data = _corpus(kind, 1 << 21, 91)
+    data = _corpus("mixed" if kind == "head" else kind, 1 << 21, 91)
+    rnd = rng.integers(0, 256, 230, dtype=np.uint8).tobytes() + bytes(200)
     frames, caps, want = [], [], []
     for i in range(3000):
         n = int(rng.choice([4096, 4096, int(rng.integers(1, 4609))]))
         s0 = int(rng.integers(0, data.size - n))
         blk = data[s0:s0 + n].tobytes()
+        if kind == "head":  # a long first sequence, then short ones (lane hand-over mid-block)
+            blk = (rnd + blk)[:n]
         f = oracle_ref.compress(blk, BYU16)[1]
         cap = n + (32 if i % 4 == 1 else 0)
         if i % 9 == 2:
@@ -345,7 +350,7 @@ def test_decompress_small_blocks_in_lds(gpu, kind):
         frames.append(f)
         caps.append(cap)
         want.append(oracle_ref.decompress(f, cap))
-    for mode in (DEC_AUTO, DEC_SMALL):
+    for mode in (DEC_AUTO, DEC_SMALL, DEC_LANE):
         r, outs = _gpu_decompress(gpu, frames, caps, max_cap=max(caps), mode=mode)
         for i, (er, eb) in enumerate(want):
             assert r[i] == er, (mode, i, r[i], er)
@@ -772,11 +777,12 @@ def test_decompress_pipelined_vs_wave_decoder(gpu, kind):
     r_ck, o_ck = _gpu_decompress(gpu, frames, caps, mode=DEC_CHUNK)
     r_rl, o_rl = _gpu_decompress(gpu, frames, caps, mode=DEC_RELAY)
     r_sm, o_sm = _gpu_decompress(gpu, frames, caps, mode=DEC_SMALL)
+    r_ln, o_ln = _gpu_decompress(gpu, frames, caps, mode=DEC_LANE)
     for i, (er, eb) in enumerate(want):
-        assert r_wg[i] == er == r_wv[i] == r_ck[i] == r_rl[i] == r_sm[i], \
-            (i, r_wg[i], er, r_wv[i], r_ck[i], r_rl[i], r_sm[i])
+        assert r_wg[i] == er == r_wv[i] == r_ck[i] == r_rl[i] == r_sm[i] == r_ln[i], \
+            (i, r_wg[i], er, r_wv[i], r_ck[i], r_rl[i], r_sm[i], r_ln[i])
         if er >= 0:
-            assert o_wg[i] == eb == o_wv[i] == o_ck[i] == o_rl[i] == o_sm[i], i
+            assert o_wg[i] == eb == o_wv[i] == o_ck[i] == o_rl[i] == o_sm[i] == o_ln[i], i
 
 
 # ---------------------------------------------------------------------------

@@ -21,7 +21,7 @@ L = lz4e_amd.lib()
 P = ctypes.c_void_p
 L.lz4e_debug_decompress_stamped.argtypes = [P] * 7 + [ctypes.c_uint32, P, P, ctypes.c_uint32,
                                                        ctypes.c_uint32]
-NAMES = {1: "one-wave", 2: "pipelined", 4: "chunked", 5: "relay", 6: "lds-small"}
+NAMES = {1: "one-wave", 2: "pipelined", 4: "chunked", 5: "relay", 6: "lds-small", 7: "lane"}
 
 
 def class_blocks(kind, n, bs):
@@ -93,3 +93,5 @@ if __name__ == "__main__":
         run("text256k", corpus.text_proxy(3815 * 262144, 0x7E57), 262144, 3, modes)
     if "fio4k" in wls:
         run("fio4k", corpus.fio_pattern(262144 * 4096), 4096, 1, modes)
+    if "sil4k" in wls:  # short sequences in small blocks
+        run("sil4k", corpus.silesia_proxy(65536 * 4096, 0x5157), 4096, 1, modes)

@@ -25,11 +25,12 @@ int launch_order_mode(bool) { return kOrderNever; }
 thread_local EmuWave* g_emu_wave;
 thread_local uint32_t g_emu_lane;
 thread_local std::barrier<>* g_emu_group;
-dim3 blockIdx;
+dim3 blockIdx, gridDim;
 thread_local dim3 threadIdx;
 
 void emu_launch(uint32_t nblocks, uint32_t threads, std::function<void()> body) {
     const uint32_t nw = (threads + 63) / 64;
+    gridDim = dim3(nblocks);
     for (uint32_t b = 0; b < nblocks; ++b) {
         blockIdx = dim3(b);
         std::unique_ptr<EmuWave[]> waves(new EmuWave[nw]);

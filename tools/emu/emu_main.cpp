@@ -9,6 +9,8 @@
 //            2 waves: parser + sequence copier)
 //   emu_main -l FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (one-wave decoder,
 //            LDS output for blocks of <= 4608 bytes without a dictionary)
+//   emu_main -n FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (lane-per-block
+//            decoder)
 // compresses one block through the unmodified kernel source, prints the
 // return value and the iterator post-state words, and writes the frame.
 // With DICT_FILE the block is compressed in dictionary mode against the
@@ -65,7 +67,7 @@ static int decode_main(int argc, char** argv) {
     frame.reserve((frame.size() + 3) & ~(size_t)3);
     // kDecPipe / kDecChunk / kDecRelay / kDecSmall / kDecWave
     const char m = argv[1][1];
-    const uint32_t mode = m == 'p' ? 2u : (m == 'c' ? 4u : (m == 'r' ? 5u : (m == 'l' ? 6u : 1u)));
+    const uint32_t mode = m == 'p' ? 2u : (m == 'c' ? 4u : (m == 'r' ? 5u : (m == 'l' ? 6u : (m == 'n' ? 7u : 1u))));
     emu_decompress_batch_mode(frame.data(), &so, &csize, out.data(), &doff, &cap, &ret, 1, &D, mode);
     char err[256];
     const int good = emu_decode_results(&ret, 1, err, sizeof err);
@@ -82,7 +84,7 @@ static int decode_main(int argc, char** argv) {
 int main(int argc, char** argv) {
     if (argc > 3 && argv[1][0] == '-' &&
         (argv[1][1] == 'd' || argv[1][1] == 'p' || argv[1][1] == 'c' || argv[1][1] == 'r' ||
-         argv[1][1] == 'l'))
+         argv[1][1] == 'l' || argv[1][1] == 'n'))
         return decode_main(argc, argv);
     if (argc < 3) {
         fprintf(stderr, "usage: emu_main BLOCK_FILE TABLE_CLASS [FRAME_OUT]\n");

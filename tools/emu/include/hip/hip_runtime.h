@@ -15,6 +15,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <stdlib.h>
+#include <string.h>
 #include <barrier>
 #include <functional>
 #include <thread>
@@ -42,9 +43,20 @@ typedef void* hipStream_t;
 inline hipError_t hipGetLastError() { return hipSuccess; }
 inline hipError_t hipMalloc(void**, size_t) { return hipErrorOutOfMemory; }
 inline hipError_t hipFree(void*) { return hipSuccess; }
-// (the launch order kernels are not emulated: no pool, block order)
-inline hipError_t hipMallocAsync(void**, size_t, hipStream_t) { return hipErrorOutOfMemory; }
-inline hipError_t hipFreeAsync(void*, hipStream_t) { return hipSuccess; }
+// Stream-ordered scratch (the lane decoder's hand-over list; the launch
+// order kernels only run for batches far larger than the emulator's).
+inline hipError_t hipMallocAsync(void** p, size_t n, hipStream_t) {
+    *p = malloc(n);
+    return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+inline hipError_t hipFreeAsync(void* p, hipStream_t) {
+    free(p);
+    return hipSuccess;
+}
+inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) {
+    memset(p, v, n);
+    return hipSuccess;
+}
 
 // ---- emulated wave / workgroup --------------------------------------------
 struct EmuWave {
@@ -54,7 +66,7 @@ struct EmuWave {
 extern thread_local EmuWave* g_emu_wave;
 extern thread_local uint32_t g_emu_lane;
 extern thread_local std::barrier<>* g_emu_group;
-extern dim3 blockIdx;
+extern dim3 blockIdx, gridDim;
 extern thread_local dim3 threadIdx;
 
 inline void emu_wave_barrier() { g_emu_wave->bar.arrive_and_wait(); }

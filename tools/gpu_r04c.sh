@@ -9,3 +9,10 @@ tail -2 gpurun_out/pytest_dec.log
 timeout -k 10 400 python -u tools/decmodes.py ${MODES:-2,5,1,6} ${WL:-silesia,text256k,fio4k} > gpurun_out/decmodes.txt 2>&1 \
   || { cat gpurun_out/decmodes.txt; exit 1; }
 grep "==\|!!" gpurun_out/decmodes.txt
+# variants (tools/build_decvar.sh): the same modes
+for f in lz4-sgori_amd/build/var/lib*.so; do
+  [ -e "$f" ] || continue
+  n=$(basename $f .so)
+  LZ4E_LIB=$PWD/$f timeout -k 10 400 python -u tools/decmodes.py ${MODES:-2,5,1,6} ${WL:-silesia,text256k,fio4k} > gpurun_out/decmodes_$n.txt 2>&1 || { cat gpurun_out/decmodes_$n.txt; exit 1; }
+  echo "-- $n"; grep "==\|!!" gpurun_out/decmodes_$n.txt
+done
