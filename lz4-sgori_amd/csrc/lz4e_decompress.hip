@@ -3173,6 +3173,12 @@ constexpr uint32_t kPipeMinCap = 16384;
 // blocks: 2.74 -> 1.53 ms; 4 KiB Silesia-proxy blocks, all handed over:
 // 1.13 -> 1.12 ms; tools/decmodes.py).
 constexpr uint32_t kLaneMinBlocks = 131072;
+// Batches of small blocks that fit one round of the LDS form's workgroups
+// (11.8 KiB of LDS: 13 per CU) take that form: no HBM round trip inside a
+// block's decode (drop-in single call, 4 KiB text: 89 -> 79 us p50); with
+// more rounds the one-wave form's 20 workgroups per CU win (65 536 4 KiB
+// Silesia-proxy blocks: 1.13 vs 1.30 ms).
+constexpr uint32_t kSmallMaxBlocks = 256 * 13;
 constexpr uint32_t kPipeMaxCap = 131072;
 
 // Launch order of the pipelined decoder when the batch takes more than one
@@ -3207,7 +3213,10 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
     if (mode == kDecAuto)
         mode = (a.max_cap == 0 || (a.max_cap >= kPipeMinCap && a.max_cap < kPipeMaxCap))
                    ? kDecPipe
-                   : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks >= kLaneMinBlocks ? kDecLane : kDecWave);
+                   : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks >= kLaneMinBlocks
+                          ? kDecLane
+                          : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks <= kSmallMaxBlocks ? kDecSmall
+                                                                                              : kDecWave));
     if (mode == kDecRelay) {
         const int om = launch_order_mode(false);
         uint32_t* order = nullptr;
