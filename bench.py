@@ -385,17 +385,20 @@ def single_call(threads_list=(1, 4, 16), calls: int = 400) -> dict:
     return res
 
 
-def block_floor(b: "Batch", top: int = 8, reps: int = 5) -> dict:
+def block_floor(b: "Batch", top: int = 4, cands: int = 32, reps: int = 5) -> dict:
     """The per-block floor of a step: the slowest blocks' compress + decode
     time with the chip to themselves.  A stamped compress pass (per-block
-    cycle counters, lz4e_debug_compress_stamped) names the `top` slowest
-    blocks; each is then compressed and decoded alone (one-block launches,
-    HIP events on the batch's stream, each pair right after a full-batch
-    compress so the lone wave runs at the clock the chip holds under this
-    workload, median of `reps`), and its stamped cycles alone are recorded
-    (a clock-free count).  However many GPUs
-    share the corpus, a step cannot be shorter than this: strong scaling's
-    ceiling is step(N=1) / floor."""
+    cycle counters, lz4e_debug_compress_stamped) names the `cands` blocks
+    with the most cycles under the full launch; each is compressed alone
+    once, stamped (its cycles with the chip to itself: a clock-free count,
+    the same on every box), and the `top` slowest by that count are then
+    compressed and decoded alone (one-block launches, HIP events on the
+    batch's stream, each pair right after a full-batch compress so the lone
+    wave runs at the clock the chip holds under this workload, median of
+    `reps`).  Choosing by the lone count, not by the full-launch count (which
+    moves with the launch's placement), keeps the chosen block the same from
+    box to box.  However many GPUs share the corpus, a step cannot be shorter
+    than this: strong scaling's ceiling is step(N=1) / floor."""
     import ctypes
 
     import torch
@@ -414,19 +417,22 @@ def block_floor(b: "Batch", top: int = 8, reps: int = 5) -> dict:
         raise SystemExit("bench: stamped compress failed: " + lz4e_amd.last_error())
     cyc = dbg.view(b.nblk, 8)[:, :6].sum(1).cpu().numpy()
     one = torch.zeros(8, dtype=torch.int64, device=b.dev)
-    worst = []
-    for i in np.argsort(cyc)[::-1][:top]:
+    lone = []
+    for i in np.argsort(cyc)[::-1][:cands]:
         i = int(i)
         sl = slice(i, i + 1)
-        # the block alone, stamped: its cycles with the chip to itself (a
-        # clock-free count: the same on every box)
+        # the block alone, stamped: its cycles with the chip to itself
         one.zero_()
         L.lz4e_debug_compress_stamped(b.d_src.data_ptr(), b.d_off[sl].data_ptr(), b.d_len[sl].data_ptr(),
                                       b.d_tt[sl].data_ptr(), b.d_dst.data_ptr(), b.d_doff[sl].data_ptr(),
                                       b.d_cap[sl].data_ptr(), b.d_ret[sl].data_ptr(), 1, b.bs,
                                       b.stream.cuda_stream, one.data_ptr())
         torch.cuda.synchronize(b.dev)
-        alone = int(one[:6].sum().item())
+        lone.append((int(one[:6].sum().item()), i))
+    lone.sort(reverse=True)
+    worst = []
+    for alone, i in lone[:top]:
+        sl = slice(i, i + 1)
         tcs, tds = [], []
         for _ in range(reps):
             # a full-batch compress right before each timed pair: the lone
@@ -458,10 +464,12 @@ def block_floor(b: "Batch", top: int = 8, reps: int = 5) -> dict:
             "block": i, "stamped_cycles_in_full_launch": c, "stamped_cycles_alone": alone,
             "clock_ghz_est": round(float(np.median(clock)), 3) if clock else None,
             "compress_ms_at_2_4ghz": round(alone / 2.4e6, 4),
-            "method": f"the {top} blocks with the most stamped compress cycles, each compressed and "
-                      f"decoded alone right after a full-batch compress (median of {reps}); the slowest "
-                      f"sum is the floor.  clock_ghz_est = the blocks' stamped cycles alone / their "
-                      f"compress time alone (launch overhead included, so a lower bound)"}
+            "max_stamped_cycles_alone": lone[0][0] if lone else None,
+            "method": f"of the {cands} blocks with the most stamped compress cycles in the full launch, "
+                      f"the {top} with the most stamped cycles alone, each compressed and decoded alone "
+                      f"right after a full-batch compress (median of {reps}); the slowest sum is the "
+                      f"floor.  clock_ghz_est = the blocks' stamped cycles alone / their compress time "
+                      f"alone (launch overhead included, so a lower bound)"}
 
 
 def decompress_only(b: "Batch", steps: int, rank: int, world: int, dist, dev, traffic_json: str,
