@@ -1958,8 +1958,12 @@ LZ4E_DEV bool copy_fast(PipeLds& S, uint32_t c, int32_t j, const Batch& b, const
 }
 
 // 6 workgroups (24 waves) per CU: 76 VGPRs and 19 KiB of LDS each.
+// (LZ4E_PIPE_MINWG: the occupancy asked of the compiler, experiments.)
+#ifndef LZ4E_PIPE_MINWG
+#define LZ4E_PIPE_MINWG 6
+#endif
 template <bool kStamps>
-__global__ __launch_bounds__(kPipeWaves * kWave, 6) void decompress_pipe_kernel(
+__global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_MINWG) void decompress_pipe_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
     const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
