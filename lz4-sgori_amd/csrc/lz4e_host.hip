@@ -427,7 +427,7 @@ int compress_sg_batch_impl(struct lz4e_sg_request* reqs, int n, const char* cons
 // lz4e_req.c:177 -> lz4e_chunk.c:139-159), and a lone block is one wave's
 // serial parse on the GPU (~0.1-0.2 ms): calls that arrive while others are
 // in flight are worth one launch together.  Leader / follower batching: a
-// caller queues its request; when fewer than kMaxInflight batches are in
+// caller queues its request; when fewer than max_inflight() batches are in
 // flight, it takes every queued request (its own included, up to kMaxBatch)
 // and runs them as one batch on its own thread -- the same batch entry point
 // as lz4e_compress_sg_batch / lz4e_decompress_batch, with identical bytes --
@@ -436,7 +436,16 @@ int compress_sg_batch_impl(struct lz4e_sg_request* reqs, int n, const char* cons
 // ---------------------------------------------------------------------------
 template <class Req>
 struct Coalescer {
-    static constexpr int kMaxInflight = 4;    // concurrent batches (= HW queues of the process)
+    static constexpr int kMaxInflightDefault = 4;  // concurrent batches (= HW queues of the process)
+    // LZ4E_COALESCE_INFLIGHT overrides it (A/B experiments)
+    static int max_inflight() {
+        static const int v = [] {
+            const char* e = getenv("LZ4E_COALESCE_INFLIGHT");
+            const int k = e ? atoi(e) : kMaxInflightDefault;
+            return k >= 1 && k <= 64 ? k : kMaxInflightDefault;
+        }();
+        return v;
+    }
     static constexpr size_t kMaxBatch = 1024;
     // A leader takes queued requests until their input reaches this (its own
     // request always goes): one caller's huge request does not make a
@@ -463,7 +472,7 @@ struct Coalescer {
             return;
         }
         while (!r->done) {
-            if (!r->taken && inflight < kMaxInflight) {
+            if (!r->taken && inflight < max_inflight()) {
                 Req* batch[kMaxBatch];
                 size_t n = 0;
                 uint64_t bytes = 0;
