@@ -1513,7 +1513,10 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
 
 // The lane-per-block decoder (see lane_decode): block b on lane b % 256 of
 // workgroup b / 256.
-constexpr uint32_t kLaneWg = 256;
+#ifndef LZ4E_LANE_WG
+#define LZ4E_LANE_WG 256
+#endif
+constexpr uint32_t kLaneWg = LZ4E_LANE_WG;
 // Residency cap: LDS the workgroup never uses, so that one 256-lane
 // workgroup runs per CU.  Fewer blocks in flight keep more of each lane's
 // lines in L2 between its accesses: fio4k 1.46-1.53 -> 1.31-1.38 ms (80 KiB,
