@@ -84,7 +84,7 @@ def test_emulated_kernel_sanitized(emu_exe, tmp_path, kind, n, cls):
     blk, frame = tmp_path / "blk.bin", tmp_path / "frame.bin"
     blk.write_bytes(data)
     out = subprocess.run([emu_exe, str(blk), str(cls), str(frame)], capture_output=True, text=True,
-                         timeout=300)
+                         timeout=1200)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "ERROR: AddressSanitizer" not in out.stderr and "runtime error" not in out.stderr
     _, r, _, fs, lr = out.stdout.split()
@@ -110,7 +110,7 @@ def test_emulated_kernel_dictionary_sanitized(emu_exe, tmp_path, kind, n, dsize)
     blk.write_bytes(blkb)
     dct.write_bytes(dic)
     out = subprocess.run([emu_exe, str(blk), str(BYU32), str(frame), str(dct)], capture_output=True,
-                         text=True, timeout=300)
+                         text=True, timeout=1200)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "ERROR: AddressSanitizer" not in out.stderr and "runtime error" not in out.stderr
     r = int(out.stdout.split()[1])
@@ -133,7 +133,7 @@ def _emu_decode(exe, tmp_path, frame, cap, dic=b"", flag="-d"):
     if o.exists():
         o.unlink()
     out = subprocess.run([exe, flag, str(f), str(cap), str(o), str(d)], capture_output=True, text=True,
-                         timeout=300)
+                         timeout=1200)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "ERROR: AddressSanitizer" not in out.stderr and "runtime error" not in out.stderr
     r = int(out.stdout.split()[1])
@@ -322,7 +322,7 @@ def _emu_decode_pipe(exe, tmp_path, frame, cap, dic=b"", flag="-p"):
     if o.exists():
         o.unlink()
     out = subprocess.run([exe, flag, str(f), str(cap), str(o), str(d)], capture_output=True, text=True,
-                         timeout=600)
+                         timeout=1200)
     assert out.returncode == 0, out.stderr[-2000:]
     assert "ERROR: AddressSanitizer" not in out.stderr and "runtime error" not in out.stderr
     lines = out.stdout.split("\n")
@@ -335,7 +335,7 @@ PIPE_CASES = [(k, m) for k in ("text", "records", "ints", "runs") for m in range
 
 # the chunked and relay decoders (modes 4 and 5, never auto-picked) on a subset
 PIPE_RUNS = [(k, m, "-p") for k, m in PIPE_CASES] + \
-    [(k, m, f) for k, m in PIPE_CASES if k in ("text", "records") for f in ("-c", "-r")]
+    [(k, m, f) for k, m in PIPE_CASES if k == "text" for f in ("-c", "-r")]
 _PN = {"-p": "pipe", "-c": "chunk", "-r": "relay"}
 
 
