@@ -3181,7 +3181,7 @@ constexpr uint32_t kPipeMinCap = 16384;
 // decoder (blocks that open with a short sequence go straight on to the
 // one-wave decoder): a lane's block takes ~1 ms, which only pays once the
 // one-wave decoder needs dozens of rounds of workgroups (fio4k, 262 144
-// blocks: 2.74 -> 1.53 ms; 4 KiB Silesia-proxy blocks, all handed over:
+// blocks: 2.74 -> 1.34-1.39 ms; 4 KiB Silesia-proxy blocks, all handed over:
 // 1.13 -> 1.12 ms; tools/decmodes.py).
 constexpr uint32_t kLaneMinBlocks = 131072;
 // Batches of small blocks that fit one round of the LDS form's workgroups
