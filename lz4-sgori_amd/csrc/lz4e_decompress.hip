@@ -3190,6 +3190,11 @@ constexpr uint32_t kLaneMinBlocks = 131072;
 // more rounds the one-wave form's 20 workgroups per CU win (65 536 4 KiB
 // Silesia-proxy blocks: 1.13 vs 1.30 ms).
 constexpr uint32_t kSmallMaxBlocks = 256 * 13;
+// Batches of at most one block per CU are latency-bound whatever the block
+// size: the pipelined decoder overlaps a block's parse with its copies
+// (drop-in single call, 4 KiB text: 71 us p50 against 82 us for the LDS form
+// and 92 us one-wave; tools/single_call_trace.py).
+constexpr uint32_t kLatencyMaxBlocks = 256;
 constexpr uint32_t kPipeMaxCap = 131072;
 
 // Launch order of the pipelined decoder when the batch takes more than one
@@ -3226,8 +3231,10 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
                    ? kDecPipe
                    : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks >= kLaneMinBlocks
                           ? kDecLane
-                          : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks <= kSmallMaxBlocks ? kDecSmall
-                                                                                              : kDecWave));
+                          : (a.nblocks <= kLatencyMaxBlocks
+                                 ? kDecPipe
+                                 : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks <= kSmallMaxBlocks ? kDecSmall
+                                                                                                     : kDecWave)));
     if (mode == kDecRelay) {
         const int om = launch_order_mode(false);
         uint32_t* order = nullptr;
