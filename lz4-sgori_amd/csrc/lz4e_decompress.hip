@@ -2,8 +2,10 @@
 //
 // Restates /root/reference/lz4e/lz4e_decompress.c:62-469
 // (LZ4E_decompress_generic, instance endOnInputSize + decode_full_block +
-// noDict).  Both decoders share one parse (parse_batch) and differ in how the
-// copies of a batch are scheduled:
+// noDict).  The batch decoders share one parse (parse_batch) and differ in
+// how the copies of a batch are scheduled; the lane decoder runs the scalar
+// loop per lane.  launch_impl picks one per launch ("Auto
+// mode, in full"):
 //
 //  * Parse, in batches of up to 64 sequences: the token stream is walked
 //    wave-uniformly with the reference's exact sequence of bound checks --
@@ -15,7 +17,7 @@
 //    else is one sequence on the exact scalar path.  Sequence k of a batch is
 //    recorded in lane k (literal source, literal length, output position,
 //    offset, match length).
-//  * decompress_kernel, one wave per block (blocks under 16 KiB): the wave
+//  * decompress_kernel, one wave per block (small and 256 KiB blocks): the wave
 //    parses a batch, then copies it -- fast batches assembled in a small LDS
 //    span (literals from a 1 KiB LDS ring that mirrors the compressed
 //    segments the parse loaded, match sources before the batch from HBM,
@@ -23,11 +25,17 @@
 //    bytes) and written with one pass of 16-byte stores; scalar-path batches
 //    (long runs, block ends) copy in HBM.  LDS per block: ring 1 KiB +
 //    mirror 128 B + store sink 256 B + span 2,112 B + jump table 4,224 B =
-//    7,744 B.
-//  * decompress_pipe_kernel, one 4-wave workgroup per block (16 KiB and up):
-//    wave 0 parses while three copier waves assemble three batches at once,
-//    cross-batch sources resolved from the spans of the two previous batches
-//    (see the section below).  19 KiB of LDS per block.
+//    7,744 B.  Its LDS form (blocks of <= 4608 bytes) stages the whole input
+//    and assembles the whole output in LDS.
+//  * decompress_pipe_kernel, one 4-wave workgroup per block (16-128 KiB, and
+//    batches of at most 256 blocks): wave 0 parses while three copier waves
+//    assemble three batches at once, cross-batch sources resolved from the
+//    spans of the two previous batches (see the section below).  19 KiB of
+//    LDS per block.
+//  * decompress_lane_kernel, one block per lane (>= 131072 blocks of <= 4608
+//    bytes), handing blocks of short sequences to decompress_resume_kernel.
+//  * decompress_chunk_kernel and decompress_relay_kernel: experiments, never
+//    picked by auto mode.
 //
 // Overlapping matches follow LZ semantics out[op + t] = out[op - off + t]
 // byte by byte; offset 0 writes zeros, which is what the reference's
