@@ -28,7 +28,7 @@
 //    7,744 B.  Its LDS form (blocks of <= 4608 bytes) stages the whole input
 //    and assembles the whole output in LDS.
 //  * decompress_pipe_kernel, one 4-wave workgroup per block (16-128 KiB, and
-//    batches of at most 256 blocks): wave 0 parses while three copier waves
+//    batches of at most 1024 blocks): wave 0 parses while three copier waves
 //    assemble three batches at once, cross-batch sources resolved from the
 //    spans of the two previous batches (see the section below).  19 KiB of
 //    LDS per block.
@@ -3198,11 +3198,14 @@ constexpr uint32_t kLaneMinBlocks = 131072;
 // more rounds the one-wave form's 20 workgroups per CU win (65 536 4 KiB
 // Silesia-proxy blocks: 1.13 vs 1.30 ms).
 constexpr uint32_t kSmallMaxBlocks = 256 * 13;
-// Batches of at most one block per CU are latency-bound whatever the block
-// size: the pipelined decoder overlaps a block's parse with its copies
-// (drop-in single call, 4 KiB text: 71 us p50 against 82 us for the LDS form
-// and 92 us one-wave; tools/single_call_trace.py).
-constexpr uint32_t kLatencyMaxBlocks = 256;
+// Batches that leave most of the pipelined decoder's round of workgroups
+// (1 536) unused are latency-bound whatever the block size: the pipelined
+// decoder overlaps a block's parse with its copies (drop-in single call,
+// 4 KiB text: 71 us p50 against 82 us for the LDS form and 92 us one-wave,
+// tools/single_call_trace.py; 1 024 4 KiB Silesia-proxy blocks 0.085 ms
+// against 0.101 / 0.102, fio 0.036 / 0.034 / 0.035; at 3 072 blocks the LDS
+// form wins, 0.115 against 0.162 ms; tools/decmodes.py).
+constexpr uint32_t kLatencyMaxBlocks = 1024;
 constexpr uint32_t kPipeMaxCap = 131072;
 
 // Launch order of the pipelined decoder when the batch takes more than one

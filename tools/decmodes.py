@@ -93,5 +93,11 @@ if __name__ == "__main__":
         run("text256k", corpus.text_proxy(3815 * 262144, 0x7E57), 262144, 3, modes)
     if "fio4k" in wls:
         run("fio4k", corpus.fio_pattern(262144 * 4096), 4096, 1, modes)
+    if "sil4k_1k" in wls:  # a batch of 1 024 small blocks (decoder choice for mid-size batches)
+        run("sil4k_1k", corpus.silesia_proxy(1024 * 4096, 0x5157), 4096, 1, modes)
+    if "fio4k_1k" in wls:
+        run("fio4k_1k", corpus.fio_pattern(1024 * 4096), 4096, 1, modes)
+    if "sil4k_3k" in wls:
+        run("sil4k_3k", corpus.silesia_proxy(3072 * 4096, 0x5157), 4096, 1, modes)
     if "sil4k" in wls:  # short sequences in small blocks
         run("sil4k", corpus.silesia_proxy(65536 * 4096, 0x5157), 4096, 1, modes)
