@@ -454,22 +454,41 @@ def block_floor(b: "Batch", top: int = 4, cands: int = 32, reps: int = 5) -> dic
             tds.append(e1.elapsed_time(e2))
         tc, td = float(np.median(tcs)), float(np.median(tds))
         worst.append((tc + td, tc, td, i, int(cyc[i]), alone))
+    # the shader clock the chip holds right after a full-batch compress:
+    # delta s_memtime / delta s_memrealtime x 100 MHz in a one-wave probe
+    # (MI355X_MICROARCH.md:503), median of `reps`
+    L.lz4e_debug_clock_probe.argtypes = [P, P, ctypes.c_uint32]
+    probe = torch.zeros(3, dtype=torch.int64, device=b.dev)
+    clock = []
+    for _ in range(reps):
+        b.compress()
+        if L.lz4e_debug_clock_probe(b.stream.cuda_stream, probe.data_ptr(), 1 << 20) != 0:
+            break
+        torch.cuda.synchronize(b.dev)
+        mt, rt = (int(v) for v in probe[:2].cpu())
+        if rt > 0:
+            clock.append(mt / rt * 0.1)
     # restore the batch's frames (the single-block launches rewrote their own)
     b.compress()
     torch.cuda.synchronize(b.dev)
     worst.sort(reverse=True)
     t, tc, td, i, c, alone = worst[0]
-    clock = [a / (x[1] * 1e6) for x in worst if (a := x[5]) > 0 and x[1] > 0]
+    ghz = float(np.median(clock)) if clock else None
     return {"floor_ms": round(t, 4), "compress_ms": round(tc, 4), "decompress_ms": round(td, 4),
             "block": i, "stamped_cycles_in_full_launch": c, "stamped_cycles_alone": alone,
-            "clock_ghz_est": round(float(np.median(clock)), 3) if clock else None,
-            "compress_ms_at_2_4ghz": round(alone / 2.4e6, 4),
+            "clock_ghz_est": round(ghz, 3) if ghz else None,
+            "clock_ghz_runs": [round(x, 3) for x in clock],
+            "stamped_ms_at_clock_est": round(alone / (ghz * 1e6), 4) if ghz else None,
             "max_stamped_cycles_alone": lone[0][0] if lone else None,
             "method": f"of the {cands} blocks with the most stamped compress cycles in the full launch, "
-                      f"the {top} with the most stamped cycles alone, each compressed and decoded alone "
-                      f"right after a full-batch compress (median of {reps}); the slowest sum is the "
-                      f"floor.  clock_ghz_est = the blocks' stamped cycles alone / their compress time "
-                      f"alone (launch overhead included, so a lower bound)"}
+                      f"the {top} with the most stamped compress cycles alone (the decode leg plays no part "
+                      f"in the choice), each compressed and decoded alone "
+                      f"right after a full-batch compress (median of {reps}); the slowest sum (the "
+                      f"unstamped kernels' HIP-event times) is the floor.  clock_ghz_est = delta "
+                      f"s_memtime / delta s_memrealtime x 100 MHz of a one-wave probe launched right "
+                      f"after a full-batch compress (median of {reps}); stamped_ms_at_clock_est = the "
+                      f"stamped cycles alone at that clock (the stamped build runs ~11 % more cycles "
+                      f"than the timed one, so it is not the floor's compress time)"}
 
 
 def decompress_only(b: "Batch", steps: int, rank: int, world: int, dist, dev, traffic_json: str,

@@ -34,8 +34,8 @@
 //    LDS per block.
 //  * decompress_lane_kernel, one block per lane (>= 131072 blocks of <= 4608
 //    bytes), handing blocks of short sequences to decompress_resume_kernel.
-//  * decompress_chunk_kernel and decompress_relay_kernel: experiments, never
-//    picked by auto mode.
+//  (The chunked and relay decoders of round 4, never picked by auto mode,
+//  were removed in round 5)
 //
 // Overlapping matches follow LZ semantics out[op + t] = out[op - off + t]
 // byte by byte; offset 0 writes zeros, which is what the reference's
@@ -1504,7 +1504,9 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
     // LDS: [input ring + mirror] [store sink] [span] [jump table]; small
     // blocks: [store sink] [output] [jump table] [input]
     constexpr uint32_t kWaveLds = kRing + kRingPad + kSink + kSpan + kJump;
-    constexpr uint32_t kSmallLds = kSink + kSmallBuf + kSmallJump + kSmallBuf;
+    // (+ 256 B after the staged input: the fast path's window probe reads up
+    // to ~258 bytes past ip, beyond any byte it uses; 12 032 B, still 13 per CU)
+    constexpr uint32_t kSmallLds = kSink + kSmallBuf + kSmallJump + kSmallBuf + 256;
     __shared__ __attribute__((aligned(16))) uint8_t smem[kSmall && kSmallLds > kWaveLds ? kSmallLds : kWaveLds];
     const int32_t dict = dict_of(dict_len, b);
     if (kSmall && dict == 0 && outSize <= kSmallOut && srcSize <= kSmallOut) {
@@ -2134,1048 +2136,6 @@ __global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_MINWG) void decompres
     }
 }
 
-// ============================================================================
-// Chunked decoder: one wave per block, a token list per 1 KiB of input
-// ============================================================================
-//
-// The two decoders above find each batch's tokens by pointer doubling over a
-// 256-byte window (five table compositions and six lookups, all dependent
-// LDS round trips, ~3.6 k cycles for ~45 text sequences), and resolve copies
-// byte by byte.  This one finds the tokens of a whole 1 KiB chunk of the
-// compressed stream at once and copies whole sequences per lane:
-//
-//  * Input window: compressed bytes [wb, wb + 2 KiB) in LDS (the chunk and
-//    the next one: a token near the chunk's end reads ahead), loaded with
-//    range-checked dword buffer loads; the next 1 KiB is prefetched into
-//    registers while the chunk's batches run.
-//  * Token walk (ck_parse): lane l walks the token chain from the start of
-//    its 16-byte segment [16 l, 16 l + 16) of the chunk -- a speculative
-//    entry -- until the chain leaves the segment: token byte, up to 3
-//    extension bytes per length field (one unaligned dword read each),
-//    next = token + 1 + ext + L + 2 + ext.  LZ4 token chains started at
-//    different positions merge within a few tokens, so nearly every lane's
-//    walk passes through the true chain's first token in its segment; the
-//    lanes whose walk does not (checked against the true entry handed over
-//    from the lane before, one shuffle per round) walk again from it.  After
-//    at most 65 rounds (each fixes the next lane; in practice 1-3) every
-//    lane's tokens from its true entry on are the reference's, and a prefix
-//    sum packs them into a list (position | L << 11 | M << 22).  A token the
-//    walk cannot take (a length-extension run of more than 3 bytes, bytes
-//    past the window, a position past iend - 18) ends the chain: the exact
-//    path takes it.
-//  * Fast batches: up to 64 listed sequences, sequence k in lane k.  The
-//    reference's checks of the sequence (lz4e_decompress.c:150-191 for a
-//    token without extension bytes; :194-220, :223-296 and :298-336 with
-//    them) are evaluated per lane with bounds strong enough that every one
-//    of them passes -- a sequence that fails them, or the batch's 1 KiB
-//    output cap, ends the batch; the exact path (ck_exact: the reference's
-//    checks in its order, one sequence, copies in HBM) decides the rest.
-//  * Output window: output bytes [ob, ob + kCkOut) in LDS.  A batch's
-//    literals are copied from the input window, the part of each match
-//    whose source lies before the batch from the window (or from HBM when it
-//    lies before ob: the window is flushed 16 bytes per lane, in order, long
-//    before its bytes leave it), and the rest -- sources inside the batch --
-//    in readiness rounds (a match is ready when its source overlaps no
-//    earlier pending match) or by pointer jumping over the batch's span when
-//    few are ready (dependency chains: records, integer tables).
-//
-// One wave owns every byte of its block, so no wave waits for another: no
-// progress counters and no watchdog.  Offset 0 writes zeros, as in the other
-// decoders (lz4e_decompress.c:313, 407-415).
-#ifndef LZ4E_CK_OUT
-#define LZ4E_CK_OUT 8192
-#endif
-#ifndef LZ4E_CK_KEEP
-#define LZ4E_CK_KEEP 4096
-#endif
-constexpr int32_t kCkChunk = 1024;            // compressed bytes per chunk
-constexpr int32_t kCkSeg = 16;                // ... per lane
-constexpr int32_t kCkIn = 2 * kCkChunk;       // input window
-constexpr int32_t kCkSlots = 6;               // tokens per segment at most (3+ bytes each)
-#ifndef LZ4E_CK_WARM
-#define LZ4E_CK_WARM 16
-#endif
-constexpr int32_t kCkWarm = LZ4E_CK_WARM;     // warm-up bytes of a speculative walk
-constexpr int32_t kCkOut = LZ4E_CK_OUT;       // output window
-constexpr int32_t kCkKeep = LZ4E_CK_KEEP;     // history kept when the window moves
-constexpr int32_t kCkCap = 1024;              // output bytes per fast batch
-constexpr int32_t kCkFlush = 2048;            // flush lag
-#ifndef LZ4E_CK_AHEAD
-#define LZ4E_CK_AHEAD 1
-#endif
-constexpr bool kCkAhead = LZ4E_CK_AHEAD;      // fields / far loads one batch ahead
-#ifndef LZ4E_CK_PJ
-#define LZ4E_CK_PJ 1
-#endif
-constexpr bool kCkPJ = LZ4E_CK_PJ;            // pointer jumping when few matches are ready
-#ifndef LZ4E_CK_PJMIN
-#define LZ4E_CK_PJMIN 8
-#endif
-constexpr uint32_t kCkPJMin = LZ4E_CK_PJMIN;  // ... and at least this many pending
-static_assert(kCkKeep >= kCkFlush + 32 && kCkOut >= kCkKeep + 2 * kCkCap && kCkOut % 16 == 0,
-              "chunked decoder window sizes");
-
-struct CkLds {
-    uint8_t in[kCkIn + 16];               // input window (+ pad for reads at its end)
-    uint32_t tok[kWave * kCkSlots];       // walk slots, then the chunk's token list
-    uint8_t out[kCkOut + 16];             // output window
-    uint16_t jump[kCkCap + 32];           // pointer jumping over a batch's span
-    uint8_t sink[kSink];                  // a dword per lane for unwanted stores
-};
-
-// List entry: window position (11 bits), literal length (11), match length
-// incl. the 4 (10).
-LZ4E_DEV int32_t ck_pos(uint32_t e) { return (int32_t)(e & 2047u); }
-LZ4E_DEV int32_t ck_L(uint32_t e) { return (int32_t)((e >> 11) & 2047u); }
-LZ4E_DEV int32_t ck_M(uint32_t e) { return (int32_t)(e >> 22); }
-// Extension bytes of a length field of value v (>= 15: 15 + 255 (k - 1) + last, last < 255).
-LZ4E_DEV int32_t ck_ext(int32_t v) { return v < 15 ? 0 : (v < 270 ? 1 : (v < 525 ? 2 : 3)); }
-
-// Extension run at p (dword e = bytes p..p+3): run length k (1..3; 0: longer)
-// and the field's value.
-LZ4E_DEV uint32_t ck_run(uint32_t e, uint32_t& v) {
-    const uint32_t k = (e & 0xFFu) != 0xFFu ? 1u : (((e >> 8) & 0xFFu) != 0xFFu ? 2u : (((e >> 16) & 0xFFu) != 0xFFu ? 3u : 0u));
-    const uint32_t kk = k ? k : 1u;
-    v = 15u + 255u * (kk - 1u) + ((e >> (8 * (kk - 1u))) & 0xFFu);
-    return k;
-}
-
-// One token at window position p: its list entry and the position of the
-// token after it; false when the walk cannot take it (an extension run of
-// more than 3 bytes, or bytes read past the window).
-LZ4E_DEV bool ck_token(const lu8* in, int32_t p, uint32_t& entry, int32_t& next) {
-    const uint32_t t = in[p];
-    uint32_t L = t >> 4, Mt = t & 15u;
-    int32_t q = p + 1;
-    bool ok = true;
-    if (L == 15) {
-        const uint32_t k = ck_run(ld4(in + q), L);
-        ok = k != 0;
-        q += (int32_t)k;
-    }
-    int32_t nx = q + (int32_t)L + 2;
-    if (ok && Mt == 15) {
-        if (nx + 4 > kCkIn) {
-            ok = false;
-        } else {
-            const uint32_t k = ck_run(ld4(in + nx), Mt);
-            ok = k != 0;
-            nx += (int32_t)k;
-        }
-    }
-    ok = ok && nx + 4 <= kCkIn;
-    entry = (uint32_t)p | (L << 11) | ((Mt + 4u) << 22);
-    next = nx;
-    return ok;
-}
-
-// The chain from p while it stays inside the segment [ss, se): every token
-// walked gets a visit bit and a slot; x is the first position at or past se,
-// or the token the walk could not take (stp).
-struct CkWalk {
-    uint32_t vis = 0, cnt = 0;
-    int32_t x = 0;
-    bool stp = false;
-};
-// A walk may start before ss (a warm-up: chains started at different
-// positions merge within a few tokens, so a walk that starts kCkWarm bytes
-// early has usually joined the true chain when it enters its segment); only
-// tokens inside the segment are recorded.
-LZ4E_DEV CkWalk ck_walk(const lu8* in, lu32* slot, int32_t p, int32_t ss, int32_t se, int32_t plim) {
-    CkWalk w;
-    while (p < se) {  // at most kCkSlots tokens recorded (+ the warm-up's)
-        uint32_t e;
-        int32_t nx;
-        if (p > plim || !ck_token(in, p, e, nx)) {
-            w.stp = true;
-            break;
-        }
-        if (p >= ss) {
-            w.vis |= 1u << (p - ss);
-            slot[w.cnt++] = e;
-        }
-        p = nx;
-    }
-    w.x = p;
-    return w;
-}
-
-// Cycle / event counters of the chunked decoder's stamped build (per block,
-// u64 x kCkSt into dbg; lane 0 accumulates).
-enum { kCkParse, kCkPRounds, kCkChunks, kCkFields, kCkCopy, kCkBatches, kCkSeqs, kCkExact, kCkNExact,
-       kCkFlushSlide, kCkRounds, kCkNPJ, kCkTotal, kCkCopyPre, kCkSt = 16 };
-struct CkSt {
-    uint64_t t = 0, a[kCkSt] = {};
-    LZ4E_DEV void lap(int k) {
-        const uint64_t now = clock64();
-        a[k] += now - t;
-        t = now;
-    }
-};
-
-// The chunk's tokens from the true entry E (window position in [0, kCkChunk)):
-// the list in S.tok[0, n), the chain's exit x (first position past the
-// chunk, or the token the walk could not take: stp).
-struct CkList {
-    int32_t n = 0, x = 0;
-    bool stp = false;
-};
-template <bool kSt>
-LZ4E_DEV CkList ck_parse(CkLds& S, int32_t E, int32_t plim, uint32_t lane, CkSt& stp) {
-    const int32_t ss = kCkSeg * (int32_t)lane, se = ss + kCkSeg;
-    const uint32_t l0 = (uint32_t)E >> 4;
-    const bool act = lane >= l0;
-    const lu8* in = (const lu8*)S.in;
-    lu32* slot = (lu32*)S.tok + kCkSlots * lane;
-    int32_t T = lane == l0 ? E : ss;  // assumed first token of the true chain in the segment
-    // where this lane's walk starts: the entry itself (lane l0, or a lane
-    // whose warm-up would reach back to it), else kCkWarm bytes early
-    int32_t st = lane == l0 ? E : (ss - kCkWarm > E ? ss - kCkWarm : E);
-    bool sf = false;                  // the true chain stopped before this segment
-    CkWalk w;
-    w.x = se;
-    if (act) w = ck_walk(in, slot, st, ss, se, plim);
-    bool settled = false;
-    // Parallel rounds settle dense chains (every lane holds tokens: the
-    // hand-over from the lane before is nearly always a position its own walk
-    // passed through) in one or two rounds.  Where the chain jumps over lanes
-    // (long literal runs) a round only carries the entry one lane further,
-    // so after kCkRounds rounds the hand-over goes lane by lane along the
-    // chain instead (one step per lane that holds a true token).
-    constexpr uint32_t kCkRounds = 3;
-    for (uint32_t it = 0; it < kCkRounds; ++it) {
-        if constexpr (kSt) stp.a[kCkPRounds]++;
-        // hand-over from the lane before: its true chain's first position in this segment
-        const int32_t pT = shfl_up(T, 1), px = shfl_up(w.x, 1);
-        const int32_t pf = shfl_up((sf ? 1 : 0) | (w.stp ? 2 : 0), 1);
-        int32_t nT = T;
-        bool nsf = sf;
-        if (lane > l0) {
-            if (pf & 1) {
-                nT = pT;
-                nsf = true;
-            } else if (pT >= ss) {  // the chain passed over the lane before
-                nT = pT;
-                nsf = false;
-            } else {
-                nT = px;
-                nsf = (pf & 2) != 0;
-            }
-        }
-        const bool cons = !act || nsf || nT >= se ||
-                          (nT >= st && ((w.vis >> (nT - ss)) & 1u)) || (w.stp && w.x == nT);
-        const bool chg = nT != T || nsf != sf;
-        if (!ballot(!cons || chg)) {
-            settled = true;
-            break;
-        }
-        T = nT;
-        sf = nsf;
-        if (!cons) {
-            st = T;
-            w = ck_walk(in, slot, T, ss, se, plim);
-        }
-    }
-    CkList r;
-    bool scanned = false;
-    if (!settled) {
-        scanned = true;
-        T = INT32_MAX;  // lanes the chain does not stop in: no tokens
-        sf = false;
-        int32_t Tu = E;
-        uint32_t l = l0;
-        r.stp = false;
-        while (l < kWave) {
-            if constexpr (kSt) stp.a[kCkPRounds]++;
-            const int32_t ssl = kCkSeg * (int32_t)l;
-            const int32_t stl = (int32_t)lane_val((uint32_t)st, l);
-            const uint32_t visl = lane_val(w.vis, l);
-            int32_t xl = (int32_t)lane_val((uint32_t)w.x, l);
-            uint32_t stpl = lane_val(w.stp ? 1u : 0u, l);
-            const bool consl = (Tu >= stl && ((visl >> (Tu - ssl)) & 1u)) || (stpl && xl == Tu);
-            if (!consl) {
-                if (lane == l) {
-                    st = Tu;
-                    w = ck_walk(in, slot, Tu, ss, se, plim);
-                }
-                xl = (int32_t)lane_val((uint32_t)w.x, l);
-                stpl = lane_val(w.stp ? 1u : 0u, l);
-            }
-            if (lane == l) T = Tu;
-            if (stpl) {
-                r.stp = true;
-                Tu = xl;
-                break;
-            }
-            Tu = xl;  // >= the next segment
-            l = (uint32_t)Tu >> 4;
-        }
-        r.x = Tu;
-    }
-    // this lane's true tokens: its slots from T on
-    uint32_t j0 = 0, nt = 0;
-    if (act && !sf && T < se) {
-        j0 = popc64(w.vis & ((1u << (T - ss)) - 1u));
-        nt = w.cnt - j0;
-    }
-    const uint32_t incl = wave_incl_add(nt);
-    const uint32_t base = incl - nt;
-    uint32_t e[kCkSlots];
-#pragma unroll
-    for (uint32_t q = 0; q < kCkSlots; ++q) e[q] = q < nt ? slot[j0 + q] : 0u;
-    lockstep();  // every lane has read its slots before the list overwrites them
-    lu32* list = (lu32*)S.tok;
-#pragma unroll
-    for (uint32_t q = 0; q < kCkSlots; ++q)
-        if (q < nt) list[base + q] = e[q];
-    lockstep();
-    r.n = (int32_t)lane_val(incl, kWave - 1);
-    if (scanned) return r;
-    // the exit: what lane 63 hands over
-    const int32_t T63 = (int32_t)lane_val((uint32_t)T, kWave - 1);
-    const int32_t x63 = (int32_t)lane_val((uint32_t)w.x, kWave - 1);
-    const uint32_t f63 = lane_val((sf ? 1u : 0u) | (w.stp ? 2u : 0u), kWave - 1);
-    if (f63 & 1u) {
-        r.x = T63;
-        r.stp = true;
-    } else if (T63 >= kWave * kCkSeg) {
-        r.x = T63;
-        r.stp = false;
-    } else {
-        r.x = x63;
-        r.stp = (f63 & 2u) != 0;
-    }
-    return r;
-}
-
-// Byte p of the block from HBM (the exact path reads the input there).
-LZ4E_DEV uint32_t ck_gbyte(const ByteBuf& ib, int32_t sh, int32_t p) {
-    const uint32_t q = vaddr((uint32_t)(p + sh));
-    return uni((buf_ld32(ib, q & ~3u) >> (8 * (q & 3u))) & 0xFFu);
-}
-// Length-extension scan in HBM, 256 bytes per step: the first position q >=
-// p0 whose byte is not 255 or that is >= plim (p0 <= plim).
-LZ4E_DEV int32_t ck_ext_stop(const ByteBuf& ib, int32_t sh, int32_t p0, int32_t plim, uint32_t lane) {
-    for (int32_t b = (p0 + sh) & ~3;; b += 4 * (int32_t)kWave) {
-        const int32_t qa = b + 4 * (int32_t)lane;
-        const uint32_t w = buf_ld32(ib, vaddr((uint32_t)qa));
-        uint32_t m = 0;
-#pragma unroll
-        for (uint32_t t = 0; t < 4; ++t) {
-            const int32_t q = qa + (int32_t)t - sh;
-            const bool stop = q >= p0 && (((w >> (8 * t)) & 0xFFu) != 0xFFu || q >= plim);
-            m |= (stop ? 1u : 0u) << t;
-        }
-        const uint64_t bm = ballot(m != 0);
-        if (bm) {
-            const uint32_t l = ctz64(bm);
-            return b + 4 * (int32_t)l + (int32_t)__builtin_ctz(lane_val(m, l)) - sh;
-        }
-    }
-}
-
-// The exact path: one sequence at ip with every check of the reference in
-// its order (lz4e_decompress.c:123-446; the same decisions as parse_batch's
-// scalar path), its copies in HBM.  Returns kParsedScalar (ip / op past the
-// sequence; P.done for the final literal run) or kParseFail (ip: the
-// reference's failing position).
-LZ4E_DEV ParseResult ck_exact(const ByteBuf& ib, int32_t sh, const uint8_t* in, int32_t& ipr, int32_t& opr,
-                              int32_t iend, int32_t oend, int32_t D, bool& done, uint8_t* gout,
-                              uint32_t lane) {
-    int32_t ip = ipr, op = opr;
-    const int32_t shortiend = iend - 14 - 2, shortoend = oend - 14 - 18;  // :100-103
-    const uint32_t token = ck_gbyte(ib, sh, ip);
-    ip++;
-    uint32_t length = token >> 4;
-    int32_t offset = 0, lit_ip, lit_op;
-    uint32_t L;
-    if (length != 15 && ip < shortiend && op <= shortoend) {
-        // two-stage shortcut (:150-191)
-        lit_ip = ip;
-        lit_op = op;
-        L = length;
-        offset = (int32_t)(ck_gbyte(ib, sh, ip + (int32_t)length) |
-                           (ck_gbyte(ib, sh, ip + (int32_t)length + 1) << 8));
-        op += (int32_t)length;
-        ip += (int32_t)length + 2;
-        length = token & 15;
-        if (length != 15 && offset >= 8 && op >= offset) {
-            length += 4;  // 18-byte shortcut copy
-            goto record;
-        }
-        goto copy_match_checks;
-    }
-    if (length == 15) {  // :194-220
-        if (ip >= iend - 15) goto fail;
-        const int32_t q = ck_ext_stop(ib, sh, ip, iend - 16, lane);
-        const uint64_t sum = (uint64_t)length + 255ull * (uint64_t)(q - ip) + ck_gbyte(ib, sh, q);
-        length = sum > kSat ? kSat : (uint32_t)sum;
-        ip = q + 1;
-    }
-    {
-        const uint32_t cpy = (uint32_t)op + length;  // :223-288
-        const uint32_t iln = (uint32_t)ip + length;
-        lit_ip = ip;
-        lit_op = op;
-        L = length;
-        if (ugt(cpy, oend - 12) || ugt(iln, iend - 8)) {
-            if (iln != (uint32_t)iend || ugt(cpy, oend)) goto fail;
-            ip += (int32_t)length;
-            op += (int32_t)length;
-            length = 0;
-            done = true;  // final literal run: no match
-            goto record;
-        }
-        ip += (int32_t)length;
-        op = (int32_t)cpy;
-    }
-    offset = (int32_t)(ck_gbyte(ib, sh, ip) | (ck_gbyte(ib, sh, ip + 1) << 8));  // :291-296
-    ip += 2;
-    length = token & 15;
-copy_match_checks:
-    if (op - offset + D < 0) goto fail;  // :299-302
-    if (length == 15) {
-        const int32_t q = ck_ext_stop(ib, sh, ip, iend - 5, lane);
-        if (q + 1 > iend - 5) {
-            ip = q + 1;
-            goto fail;
-        }
-        const uint64_t sum = (uint64_t)length + 255ull * (uint64_t)(q - ip) + ck_gbyte(ib, sh, q);
-        length = sum > kSat ? kSat : (uint32_t)sum;
-        ip = q + 1;
-    }
-    if (ugt((uint32_t)op + length + 4, oend - 5)) goto fail;
-    length += 4;
-record:
-    {
-        Batch b;
-        const bool me = lane == 0;
-        b.ls = me ? lit_ip : 0;
-        b.L = me ? (int32_t)L : 0;
-        b.op = me ? lit_op : 0;
-        b.off = me ? offset : 0;
-        b.M = me ? (int32_t)length : 0;
-        b.n = 1;
-        copy_scalar_hbm<4>(b, in, iend, gout, oend, lane);
-    }
-    ipr = ip;
-    opr = op + (int32_t)length;
-    return kParsedScalar;
-fail:
-    ipr = ip;
-    return kParseFail;
-}
-
-// Block state of the chunked decoder (wave-uniform).
-struct CkState {
-    int32_t wb, ob, fl, op;  // input window base, output window base, flushed prefix, output position
-};
-// The LDS the output side works in: the output window, the pointer-jumping
-// table of a batch's span, the store sink.
-struct CkOut {
-    lu8* W;
-    lu16* jump;
-    lu8* sink;  // a dword per lane
-};
-
-// Store output [fl, to) (to a multiple of 16, or exact when tail) from the window.
-LZ4E_DEV void ck_flush(const CkOut& O, uint8_t* gout, CkState& C, int32_t to, bool tail, uint32_t lane) {
-    const lu8* W = O.W;
-    const int32_t t16 = to & ~15;
-    for (int32_t x = C.fl + 16 * (int32_t)lane; x < t16; x += 16 * (int32_t)kWave) {
-        const u32x4 v = *(const lu128*)(W + (x - C.ob));
-        stg16(gout + x, make_uint4(v.x, v.y, v.z, v.w));
-    }
-    if (tail && (int32_t)lane < to - t16 && t16 >= C.fl) *(gu8*)(gout + t16 + lane) = W[t16 - C.ob + lane];
-    C.fl = tail ? to : (t16 > C.fl ? t16 : C.fl);
-}
-
-// The output window base for a batch that starts at op: unchanged while
-// the batch fits, else moved to keep the last kCkKeep bytes -- never past
-// the flushed prefix (everything before ob must be in HBM).
-LZ4E_DEV int32_t ck_ob_for(const CkState& C, int32_t op) {
-    if (op + kCkCap <= C.ob + kCkOut) return C.ob;
-    const int32_t a = (op - kCkKeep) & ~15, f = C.fl & ~15;
-    const int32_t nob = a < f ? a : f;
-    return nob > C.ob ? nob : C.ob;
-}
-// Moves the output window forward to nob (> C.ob).
-LZ4E_DEV void ck_slide(const CkOut& O, CkState& C, int32_t nob, uint32_t lane) {
-    lu8* W = O.W;
-    const int32_t d = nob - C.ob, end = (C.op + 15) & ~15;
-    // forward in 1 KiB steps: step s writes [1024 s, +1024), reads d bytes
-    // further on -- never a range an earlier step wrote
-    for (int32_t x0 = 0; nob + x0 < end; x0 += 16 * (int32_t)kWave) {
-        const int32_t x = x0 + 16 * (int32_t)lane;
-        const bool act = nob + x < end;
-        u32x4 v = {0, 0, 0, 0};
-        if (act) v = *(const lu128*)(W + d + x);
-        lockstep();
-        if (act) *(lu128*)(W + x) = v;
-    }
-    lockstep();
-    C.ob = nob;
-}
-
-// Whole-wave copies of one long piece (a sequence's literal run or match
-// part longer than kCkLong), 4 bytes per lane per step.  Source and
-// destination do not overlap (the input window, bytes before the batch, or
-// HBM bytes before the window).
-constexpr int32_t kCkLong = 32;
-LZ4E_DEV void ck_wave_copy(lu8* dst, const lu8* src, int32_t n, uint32_t lane) {
-    for (int32_t t0 = 0; t0 < n; t0 += 4 * (int32_t)kWave) {
-        const int32_t t = t0 + 4 * (int32_t)lane;
-        if (t + 4 <= n) st4(dst + t, ld4(src + t));
-        else
-            for (int32_t q = t; q < n; ++q) dst[q] = src[q];
-    }
-}
-LZ4E_DEV void ck_wave_fetch(lu8* dst, const uint8_t* src, int32_t n, uint32_t lane) {
-    for (int32_t t0 = 0; t0 < n; t0 += 4 * (int32_t)kWave) {
-        const int32_t t = t0 + 4 * (int32_t)lane;
-        if (t + 4 <= n) st4(dst + t, *(const gu32w*)(src + t));
-        else
-            for (int32_t q = t; q < n; ++q) dst[q] = *(const gu8*)(src + q);
-    }
-}
-// dst[t] = dst[t - off] for t < n in LZ order (any overlap; offset 0 writes
-// zeros): steps of at most D bytes read D bytes back, D a multiple of off
-// that doubles while 2 D <= t, so every step reads bytes written before it.
-LZ4E_DEV void ck_wave_match(lu8* dst, int32_t off, int32_t n, uint32_t lane) {
-    if (off == 0) {
-        for (int32_t t0 = 0; t0 < n; t0 += 4 * (int32_t)kWave) {
-            const int32_t t = t0 + 4 * (int32_t)lane;
-            if (t + 4 <= n) st4(dst + t, 0u);
-            else
-                for (int32_t q = t; q < n; ++q) dst[q] = 0;
-        }
-        return;
-    }
-    int32_t D = off;
-    for (int32_t t0 = 0; t0 < n;) {
-        int32_t c = n - t0 < 4 * (int32_t)kWave ? n - t0 : 4 * (int32_t)kWave;
-        c = c < D ? c : D;
-        const int32_t t = 4 * (int32_t)lane;
-        if (t + 4 <= c) st4(dst + t0 + t, ld4(dst + t0 + t - D));
-        else
-            for (int32_t q = t; q < c; ++q) dst[t0 + q] = dst[t0 + q - D];
-        lockstep();  // the next step reads these bytes
-        t0 += c;
-        while (2 * D <= t0) D *= 2;
-    }
-}
-
-// A fast batch: list entries [i, i + nf), sequence k in lane k, copied
-// under the output window base ob.  Its fields -- and the HBM part of its
-// early match sources -- are computed / loaded one batch ahead (ck_fields
-// for batch j + 1 runs before batch j's copies), so the HBM latency of far
-// sources hides under the previous batch's rounds.
-struct CkBatch {
-    int32_t i = -1, nf = 0, hi = 0, ob = 0;  // (wave-uniform)
-    int32_t o = 0, L = 0, M = 0, lp = 0, off = 0, n0 = 0, nh = 0;
-    uint4 h0 = {0, 0, 0, 0}, h1 = {0, 0, 0, 0};
-};
-// The part of each match whose source lies before the batch (lo): final,
-// from the window, or from HBM before B.ob (flushed: ob <= fl) -- those
-// loads issued here, consumed by ck_copy.
-LZ4E_DEV void ck_early(CkBatch& B, int32_t lo, const uint8_t* gout, uint32_t lane) {
-    const bool valid = (int32_t)lane < B.nf;
-    const int32_t m = B.o + B.L, ss = m - B.off, ob = B.ob;
-    int32_t n0 = 0, nh = 0;
-    uint4 h0 = make_uint4(0, 0, 0, 0), h1 = h0;
-    if (valid && B.off != 0 && ss < lo) {
-        n0 = B.M < lo - ss ? B.M : lo - ss;
-        nh = ss < ob ? (n0 < ob - ss ? n0 : ob - ss) : 0;
-        if (nh > 0 && nh <= kCkLong) {
-            h0 = ldg16(gout + ss);
-            if (nh > 16) h1 = ldg16(gout + ss + 16);
-        }
-    }
-    B.n0 = n0;
-    B.nh = nh;
-    B.h0 = h0;
-    B.h1 = h1;
-}
-LZ4E_DEV void ck_fields(CkLds& S, int32_t wb, int32_t i, int32_t n, int32_t op, int32_t ob, int32_t iend,
-                        int32_t oend, int32_t D, const uint8_t* gout, uint32_t lane, CkBatch& B) {
-    const lu8* in = (const lu8*)S.in;
-    const int32_t idx = i + (int32_t)lane;
-    const bool have = idx < n;
-    const uint32_t e = have ? ((const lu32*)S.tok)[idx] : 0u;
-    const int32_t p = ck_pos(e), L = ck_L(e), M = ck_M(e);
-    const int32_t lp = p + 1 + ck_ext(L);
-    const int32_t off = have ? (int32_t)(ld4(in + lp + L) & 0xFFFFu) : 0;
-    const int32_t nx = lp + L + 2 + ck_ext(M - 4);
-    const int32_t size = have ? L + M : 0;
-    const int32_t incl = (int32_t)wave_incl_add((uint32_t)size);
-    const int32_t o = op + incl - size, m = o + L;
-    const bool ext = L >= 15 || M >= 19;
-    // every check of the reference on this sequence passes (header comment)
-    bool fast;
-    if (ext)
-        fast = wb + nx <= iend - 17 && o + size <= oend - 32 && m - off + D >= 0;
-    else
-        fast = wb + p <= iend - 18 && o <= oend - 32 &&
-               (m >= off ? (off >= 8 || m + M <= oend - 5) : (m - off + D >= 0 && m + M <= oend - 5));
-    const bool ok = have && fast && incl <= kCkCap;
-    const uint64_t okm = ballot(ok);
-    const uint32_t nf = (~okm) ? ctz64(~okm) : kWave;
-    B.i = i;
-    B.nf = (int32_t)nf;
-    B.ob = ob;
-    if (nf == 0) return;
-    const bool valid = lane < nf;
-    const int32_t lo = op;
-    B.hi = op + (int32_t)lane_val((uint32_t)incl, nf - 1);
-    B.o = o;
-    B.L = L;
-    B.M = M;
-    B.lp = lp;
-    B.off = off;
-    (void)valid;
-    ck_early(B, lo, gout, lane);
-}
-
-// The copies of batch B into the output window (C.ob == B.ob).
-// (literal sources: in + lp, in LDS)
-template <bool kSt>
-LZ4E_DEV void ck_copy(const CkOut& O, const lu8* in, const CkBatch& B, int32_t oend, uint8_t* gout,
-                      uint32_t lane, CkSt& stp) {
-    lu8* W = O.W;
-    lu8* sink = O.sink + 4 * lane;
-    const bool valid = (int32_t)lane < B.nf;
-    const int32_t ob = B.ob, lo = lane_val((uint32_t)B.o, 0), hi = B.hi;
-    const int32_t o = B.o, L = B.L, M = B.M, lp = B.lp, off = B.off, n0 = B.n0, nh = B.nh;
-    const int32_t m = o + L, ss = m - off;
-    const uint4 h0 = B.h0, h1 = B.h1;
-    // short pieces per lane, long ones (fio's 256-byte runs, long literals)
-    // by the whole wave, one piece after the other
-    const int32_t nw = n0 - nh;
-    const bool longL = valid && L > kCkLong, longW = nw > kCkLong, longH = nh > kCkLong;
-    if (valid && L > 0 && !longL) lane_copy(W + (o - ob), in + lp, L, sink);
-    if (nw > 0 && !longW) lane_copy(W + (m + nh - ob), W + (ss + nh - ob), nw, sink);
-    if (nh > 0 && !longH) {
-        put16(W + (m - ob), h0, nh < 16 ? (uint32_t)nh : 16u, sink);
-        if (nh > 16) put16(W + (m + 16 - ob), h1, (uint32_t)(nh - 16), sink);
-    }
-    for (uint64_t lm = ballot(longL); lm; lm &= lm - 1) {
-        const uint32_t k = ctz64(lm);
-        ck_wave_copy(W + ((int32_t)lane_val((uint32_t)o, k) - ob), in + lane_val((uint32_t)lp, k),
-                     (int32_t)lane_val((uint32_t)L, k), lane);
-    }
-    for (uint64_t lm = ballot(longW); lm; lm &= lm - 1) {
-        const uint32_t k = ctz64(lm);
-        const int32_t km = (int32_t)lane_val((uint32_t)m, k), kss = (int32_t)lane_val((uint32_t)ss, k);
-        const int32_t knh = (int32_t)lane_val((uint32_t)nh, k);
-        ck_wave_copy(W + (km + knh - ob), W + (kss + knh - ob), (int32_t)lane_val((uint32_t)nw, k), lane);
-    }
-    for (uint64_t lm = ballot(longH); lm; lm &= lm - 1) {
-        const uint32_t k = ctz64(lm);
-        const int32_t km = (int32_t)lane_val((uint32_t)m, k), kss = (int32_t)lane_val((uint32_t)ss, k);
-        ck_wave_fetch(W + (km - ob), gout + kss, (int32_t)lane_val((uint32_t)nh, k), lane);
-    }
-    lockstep();  // literals and early match parts, read by other lanes next
-    if constexpr (kSt) stp.lap(kCkCopyPre);
-    // the rest: sources inside the batch
-    const int32_t a0 = lo & ~15;
-    lu8* span = W + (a0 - ob);
-    const int32_t ms2 = m + n0, m2 = M - n0, me = m + M;
-    const int32_t ss2 = ss + n0;
-    const int32_t need = me - off < ms2 ? me - off : ms2;  // source part before own output
-    uint64_t pending = ballot(valid && m2 > 0);
-    while (pending) {
-        if constexpr (kSt) stp.a[kCkRounds]++;
-        const bool mine = (pending >> lane) & 1;
-        const int32_t mn = wave_excl_min(mine ? ms2 : INT32_MAX);
-        const int32_t mx = wave_excl_max(mine ? me : INT32_MIN);
-        const bool ready = mine && (need <= mn || ss2 >= mx);
-        const uint64_t rm = ballot(ready);
-        const uint32_t np = popc64(pending);
-        // pointer jumping pays only for chains of many short matches (records,
-        // integer tables); long matches (fio's 256-byte runs) go in rounds
-        if (kCkPJ && np >= kCkPJMin && 4 * popc64(rm) <= np && !ballot(mine && m2 > 2 * kCkLong)) {
-            if constexpr (kSt) stp.a[kCkNPJ]++;
-            const int32_t s0 = (int32_t)lane_val((uint32_t)ms2, ctz64(pending)) - a0;
-            resolve_chains(span, O.jump, lo - a0, hi - a0, s0, mine, ms2 - a0, m2, off, lane);
-            break;
-        }
-        const bool lng = m2 > 2 * kCkLong;
-        if (ready && !lng) {
-            if (off != 0) lane_match(span + (ms2 - a0), (uint32_t)off, m2, sink);
-            else lane_zero(span + (ms2 - a0), m2, sink);
-        }
-        lockstep();
-        for (uint64_t lm = ballot(ready && lng); lm; lm &= lm - 1) {
-            const uint32_t k = ctz64(lm);
-            ck_wave_match(span + ((int32_t)lane_val((uint32_t)ms2, k) - a0), (int32_t)lane_val((uint32_t)off, k),
-                          (int32_t)lane_val((uint32_t)m2, k), lane);
-        }
-        pending &= ~rm;
-    }
-    lockstep();
-}
-
-// Loads 1 KiB of the block's input (window position r, block position pb) as
-// 4 dwords per lane; positions past the block read as 0.
-struct CkPf {
-    uint32_t w[4];
-};
-LZ4E_DEV CkPf ck_fetch(const ByteBuf& ib, int32_t sh, int32_t pb, uint32_t lane) {
-    CkPf f;
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) f.w[j] = buf_ld32(ib, vaddr((uint32_t)(pb + sh + 4 * (int32_t)(lane + kWave * j))));
-    return f;
-}
-LZ4E_DEV void ck_put(CkLds& S, int32_t r, const CkPf& f, uint32_t lane) {
-    lu32* w = (lu32*)(S.in + r);
-#pragma unroll
-    for (uint32_t j = 0; j < 4; ++j) w[lane + kWave * j] = f.w[j];
-}
-
-template <bool kSt>
-LZ4E_DEV void ck_decode(CkLds& S, const uint8_t* in, int32_t srcSize, uint8_t* gout, int32_t outSize,
-                        int32_t D, int32_t* ret_slot, uint32_t lane, uint64_t* dbg) {
-    CkSt st;
-    if constexpr (kSt) st.t = clock64();
-    const uint64_t t00 = kSt ? st.t : 0;
-    auto finish = [&]() {
-        if constexpr (kSt) {
-            st.a[kCkTotal] = clock64() - t00;
-            if (lane == 0 && dbg)
-                for (int k = 0; k < kCkSt; ++k) dbg[k] = st.a[k];
-        }
-    };
-    const int32_t sh = (int32_t)(reinterpret_cast<uintptr_t>(in) & 3);
-    const ByteBuf ib = buf_make(in - sh, (uint32_t)((srcSize + sh + 3) & ~3));
-    const int32_t iend = srcSize, oend = outSize;
-    CkState C{-sh, 0, 0, 0};
-    const CkOut O{(lu8*)S.out, (lu16*)S.jump, (lu8*)S.sink};
-    bool wvalid = false;
-    int32_t ip = 0, n = 0, i = 0, X = 0;
-    bool stopped = false;
-    CkPf pf;
-    bool pfv = false;
-    for (uint32_t b = 0; b < 4; ++b) pf.w[b] = 0;
-    CkBatch Bn;  // the next batch's fields, computed ahead (Bn.i < 0: none)
-    for (;;) {
-        bool exact = false;
-        if (i < n) {
-            if constexpr (kSt) st.lap(kCkFlushSlide);
-            CkBatch Bt;
-            if (Bn.i == i) Bt = Bn;
-            else ck_fields(S, C.wb, i, n, C.op, ck_ob_for(C, C.op), iend, oend, D, gout, lane, Bt);
-            Bn.i = -1;
-            if constexpr (kSt) st.lap(kCkFields);
-            if (Bt.nf == 0) {
-                ip = C.wb + ck_pos(uni(((const lu32*)S.tok)[i]));
-                i++;
-                exact = true;
-            } else {
-                if (Bt.ob != C.ob) ck_slide(O, C, Bt.ob, lane);
-                if constexpr (kSt) st.lap(kCkFlushSlide);
-                const int32_t i2 = i + Bt.nf;
-                if (kCkAhead && i2 < n)
-                    ck_fields(S, C.wb, i2, n, Bt.hi, ck_ob_for(C, Bt.hi), iend, oend, D, gout, lane, Bn);
-                if constexpr (kSt) {
-                    st.lap(kCkFields);
-                    st.a[kCkBatches]++;
-                    st.a[kCkSeqs] += (uint64_t)Bt.nf;
-                }
-                ck_copy<kSt>(O, (const lu8*)S.in, Bt, oend, gout, lane, st);
-                if constexpr (kSt) st.lap(kCkCopy);
-                C.op = Bt.hi;
-                i = i2;
-                ip = C.wb + (i < n ? ck_pos(uni(((const lu32*)S.tok)[i])) : X);
-                if ((C.op & ~15) - C.fl >= kCkFlush) ck_flush(O, gout, C, C.op, false, lane);
-                if (i < n || !stopped) continue;
-                exact = true;  // the chain's stop: the exact path
-                n = 0;
-            }
-        } else if (ip > iend - 18) {
-            exact = true;  // past the fast region
-        } else {
-            // next chunk: the window must hold [ip, ip + 1 KiB) as its first half
-            const int32_t r = ip - C.wb;
-            if (wvalid && r >= kCkChunk && r < kCkIn) {
-                lu32* w = (lu32*)S.in;
-                uint32_t v[4];
-#pragma unroll
-                for (uint32_t j = 0; j < 4; ++j) v[j] = w[kCkChunk / 4 + lane + kWave * j];
-                lockstep();
-#pragma unroll
-                for (uint32_t j = 0; j < 4; ++j) w[lane + kWave * j] = v[j];
-                C.wb += kCkChunk;
-                if (!pfv) pf = ck_fetch(ib, sh, C.wb + kCkChunk, lane);
-                ck_put(S, kCkChunk, pf, lane);
-            } else if (!wvalid || r < 0 || r >= kCkChunk) {
-                C.wb = ((ip + sh) & ~3) - sh;
-                ck_put(S, 0, ck_fetch(ib, sh, C.wb, lane), lane);
-                ck_put(S, kCkChunk, ck_fetch(ib, sh, C.wb + kCkChunk, lane), lane);
-                wvalid = true;
-            }
-            pfv = false;
-            lockstep();
-            if constexpr (kSt) st.lap(kCkFlushSlide);
-            const CkList Lst = ck_parse<kSt>(S, ip - C.wb, iend - 18 - C.wb, lane, st);
-            // the next KiB, consumed when the window moves on
-            pf = ck_fetch(ib, sh, C.wb + kCkIn, lane);
-            pfv = true;
-            n = Lst.n;
-            i = 0;
-            X = Lst.x;
-            stopped = Lst.stp;
-            if constexpr (kSt) {
-                st.lap(kCkParse);
-                st.a[kCkChunks]++;
-            }
-            if (n > 0) continue;
-            if (!stopped) {
-                ip = C.wb + X;
-                continue;
-            }
-            ip = C.wb + X;
-            exact = true;
-        }
-        if (exact) {
-            if constexpr (kSt) st.lap(kCkFlushSlide);
-            // every byte before op into HBM, then one sequence there
-            ck_flush(O, gout, C, C.op, true, lane);
-            wave_fence();
-            bool done = false;
-            int32_t op = C.op;
-            const ParseResult pr = ck_exact(ib, sh, in, ip, op, iend, oend, D, done, gout, lane);
-            if constexpr (kSt) {
-                st.lap(kCkExact);
-                st.a[kCkNExact]++;
-            }
-            if (pr == kParseFail) {
-                if (lane == 0) *ret_slot = -ip - 1;
-                finish();
-                return;
-            }
-            if (done) {
-                if (lane == 0) *ret_slot = op;
-                finish();
-                return;
-            }
-            // the window restarts at the last 16-byte boundary
-            C.op = op;
-            C.ob = C.fl = op & ~15;
-            wave_fence();
-            if ((int32_t)lane < op - C.ob) ((lu8*)S.out)[lane] = *(const gu8*)(gout + C.ob + lane);
-            lockstep();
-            if (!(i < n && C.wb + ck_pos(uni(((const lu32*)S.tok)[i])) == ip)) {
-                n = 0;
-                i = 0;
-                stopped = false;
-            }
-        }
-    }
-}
-
-template <bool kStamps>
-__global__ __launch_bounds__(64) void decompress_chunk_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
-    const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
-    const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
-    uint64_t* __restrict__ dbg, const int32_t* __restrict__ dict_len,
-    const uint32_t* __restrict__ order) {
-    __shared__ __attribute__((aligned(16))) CkLds S;
-    if (blockIdx.x >= nblocks) return;
-    const uint32_t b = order ? order[blockIdx.x] : blockIdx.x;
-    const uint32_t lane = lane_id();
-    const int32_t srcSize = src_len[b];
-    const int32_t outSize = dst_cap[b];
-    const uint8_t* in = src + src_off[b];
-    uint8_t* out = dst + dst_off[b];
-    if (special_case(in, srcSize, outSize, ret + b, lane)) return;
-    ck_decode<kStamps>(S, in, srcSize, out, outSize, dict_of(dict_len, b), ret + b, lane,
-                       kStamps && dbg ? dbg + kStSlots * (size_t)b : nullptr);
-}
-constexpr uint32_t kCkPerCu = (160u * 1024u) / sizeof(CkLds);
-
-// ============================================================================
-// Relay decoder: a parser wave and a sequence-copier wave per block (mode 5)
-// ============================================================================
-//
-// Wave 0 parses exactly as the pipelined decoder does (parse_batch: the
-// reference's checks in its order, so the return value is decided there)
-// and publishes each batch -- per-lane records, output range and, for a
-// fast batch, the 512 input bytes of its parse window (the literals' source)
-// -- in a ring of record slots.  Wave 1 copies the batches in order into the
-// chunked decoder's LDS output window with its copy stage (ck_copy: whole
-// sequences per lane; the part of a match whose source lies before the batch
-// from the window, or from HBM before it; readiness rounds / pointer jumping
-// inside the batch), flushes the window to HBM 16 bytes per lane, and copies
-// a scalar-path batch (long runs, the block's final literals) in HBM after
-// flushing the whole window.  Every earlier batch is final when the copier
-// takes batch j -- one wave writes every output byte in order -- so there is
-// no cross-batch protocol beyond the record slots.  Waits are bounded by the
-// watchdog (LZ4E_DECODE_ABORTED), as in the pipelined decoder.
-#ifndef LZ4E_RELAY_RECS
-#define LZ4E_RELAY_RECS 4
-#endif
-constexpr uint32_t kRRecs = LZ4E_RELAY_RECS;
-enum { kRN, kRKind, kRLo, kRHi, kRBase, kRWords = 8 };
-struct RelayLds {
-    uint32_t ring[(kRing + kRingPad) / 4];  // parser input ring
-    int32_t rec[kRRecs][5][kWave];          // ls, L, op, off, M per sequence
-    int32_t hdr[kRRecs][kRWords];
-    uint32_t inp[kRRecs][2 * kWave];        // a fast batch's input window A|B (512 B)
-    uint8_t out[kCkOut + 16];               // output window
-    uint16_t jump[kCkCap + 32];             // pointer jumping over a batch's span
-    uint8_t sink[kSink];
-    int32_t pub[kRRecs], con[kRRecs];       // record slot published / consumed (batch index)
-    int32_t nb_total, abort, beat, result;
-};
-
-template <bool kStamps>
-__global__ __launch_bounds__(2 * kWave) void decompress_relay_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
-    const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
-    const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
-    uint64_t* __restrict__ dbg, const int32_t* __restrict__ dict_len,
-    const uint32_t* __restrict__ order) {
-    __shared__ __attribute__((aligned(16))) RelayLds S;
-    if (blockIdx.x >= nblocks) return;
-    const uint32_t b = order ? order[blockIdx.x] : blockIdx.x;
-    const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
-    const int32_t srcSize = src_len[b];
-    const int32_t outSize = dst_cap[b];
-    const uint8_t* in = src + src_off[b];
-    uint8_t* gout = dst + dst_off[b];
-    (void)dbg;
-    if (special_case(in, srcSize, outSize, ret + b, tid)) return;
-    if (tid < kRRecs) {
-        S.pub[tid] = -1;
-        S.con[tid] = (int32_t)tid - (int32_t)kRRecs;
-    }
-    if (tid == 0) {
-        S.nb_total = INT32_MAX;
-        S.abort = 0;
-        S.beat = 0;
-        S.result = kPipeAbort;
-    }
-    __syncthreads();
-
-    if (wave == 0) {
-        // ---------------- parser ----------------
-        __builtin_amdgcn_s_setprio(3);
-        Parse P;
-        P.init(in, srcSize, outSize, (lu32*)S.ring, lane, dict_of(dict_len, b));
-        int32_t j = 0;
-        for (;;) {
-            Batch bt;
-            const int32_t lo = P.op;
-            const ParseResult pr = parse_batch<true>(P, bt, lane, kCkCap);
-            if (pr == kParseFail) {
-                if (lane == 0) S.result = -P.ip - 1;
-                break;
-            }
-            const uint32_t slot = (uint32_t)j % kRRecs;
-            if (!wait_for(S, [&] { return lds_acquire(&S.con[slot]) == j - (int32_t)kRRecs; },
-                          [&] { return lds_acquire(&S.beat) + lds_acquire(&S.con[slot]); })) {
-                lds_release(&S.abort, 1);
-                break;
-            }
-            S.rec[slot][0][lane] = bt.ls;
-            S.rec[slot][1][lane] = bt.L;
-            S.rec[slot][2][lane] = bt.op;
-            S.rec[slot][3][lane] = bt.off;
-            S.rec[slot][4][lane] = bt.M;
-            if (pr == kParsedFast) {
-                S.inp[slot][lane] = P.win.a;
-                S.inp[slot][kWave + lane] = P.win.b;
-            }
-            if (lane < kRWords) {
-                const int32_t h[kRWords] = {(int32_t)bt.n, pr == kParsedScalar ? kKindHbm : kKindFast,
-                                            lo, P.op, P.win.base, 0, 0, 0};
-                int32_t v = 0;
-#pragma unroll
-                for (uint32_t q = 0; q < kRWords; ++q) v = lane == q ? h[q] : v;
-                S.hdr[slot][lane] = v;
-            }
-            lds_release(&S.pub[slot], j);
-            j++;
-            if (P.done) {
-                if (lane == 0) S.result = P.op;
-                break;
-            }
-        }
-        lds_release(&S.nb_total, j);
-    } else {
-        // ---------------- copier ----------------
-        __builtin_amdgcn_s_setprio(2);
-        const CkOut O{(lu8*)S.out, (lu16*)S.jump, (lu8*)S.sink};
-        CkState C{0, 0, 0, 0};
-        CkSt st;
-        auto beat = [&] {
-            // (called in lane-divergent loops: lane 0 alone, no ordering)
-            if (lane == 0) __hip_atomic_fetch_add(&S.beat, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        };
-        for (int32_t j = 0;; ++j) {
-            const uint32_t slot = (uint32_t)j % kRRecs;
-            const bool ok = wait_for(
-                S, [&] { return lds_acquire(&S.pub[slot]) == j || lds_acquire(&S.nb_total) <= j; },
-                [&] { return lds_acquire(&S.beat) + lds_acquire(&S.pub[slot]); });
-            if (!ok) {
-                lds_release(&S.abort, 1);
-                break;
-            }
-            if (lds_acquire(&S.pub[slot]) != j) break;  // the parser ended before batch j
-            const int32_t ls = S.rec[slot][0][lane], L = S.rec[slot][1][lane], o = S.rec[slot][2][lane];
-            const int32_t off = S.rec[slot][3][lane], M = S.rec[slot][4][lane];
-            int32_t hdr[kRWords];
-#pragma unroll
-            for (uint32_t q = 0; q < kRWords; ++q) hdr[q] = (int32_t)uni((uint32_t)S.hdr[slot][q]);
-            const int32_t lo = hdr[kRLo], hi = hdr[kRHi];
-            if (hdr[kRKind] == kKindHbm) {
-                // every window byte into HBM, then the sequence in place
-                ck_flush(O, gout, C, C.op, true, lane);
-                wave_fence();
-                Batch bt;
-                bt.ls = ls;
-                bt.L = L;
-                bt.op = o;
-                bt.off = off;
-                bt.M = M;
-                bt.n = 1;
-                lds_release(&S.con[slot], j);
-                copy_scalar_hbm<4>(bt, in, srcSize, gout, outSize, lane, beat);
-                // the window restarts at the last 16-byte boundary
-                C.op = hi;
-                C.ob = C.fl = hi & ~15;
-                wave_fence();
-                if ((int32_t)lane < hi - C.ob) O.W[lane] = *(const gu8*)(gout + C.ob + lane);
-                lockstep();
-                continue;
-            }
-            CkBatch B;
-            B.i = j;
-            B.nf = hdr[kRN];
-            B.hi = hi;
-            B.ob = ck_ob_for(C, lo);
-            B.o = o;
-            B.L = L;
-            B.M = M;
-            B.lp = ls;
-            B.off = off;
-            if (B.ob != C.ob) ck_slide(O, C, B.ob, lane);
-            ck_early(B, lo, gout, lane);
-            ck_copy<false>(O, (const lu8*)S.inp[slot] - hdr[kRBase], B, outSize, gout, lane, st);
-            lds_release(&S.con[slot], j);
-            C.op = hi;
-            if ((C.op & ~15) - C.fl >= kCkFlush) ck_flush(O, gout, C, C.op, false, lane);
-        }
-        // (the final literals are a scalar-path batch: nothing is left in the window)
-        ck_flush(O, gout, C, C.op, true, lane);
-    }
-    __syncthreads();
-    if (tid == 0) ret[b] = __hip_atomic_load(&S.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                               ? kPipeAbort
-                               : S.result;
-}
-
 // Blocks whose capacity lies in [kPipeMinCap, kPipeMaxCap) take the
 // pipelined decoder.  Small blocks parse in a few batches, and one wave each
 // keeps more of them resident.  Large blocks (256 KiB: ~560 batches each)
@@ -3228,15 +2188,21 @@ struct DecodeWeight {
 template <bool kStamps>
 hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* dbg) {
     if (a.nblocks == 0) return hipSuccess;
-    // LZ4E_DECOMPRESS_MODE=wave|pipe overrides the choice (A/B experiments).
+    // LZ4E_DECOMPRESS_MODE=w|p|s|l (one-wave, pipelined, LDS form, lane)
+    // overrides the choice for A/B experiments; any other value is auto.
+    // Auto, in order: capacity 16-128 KiB (or unknown) -> pipelined; blocks
+    // of <= kSmallOut bytes in batches of >= kLaneMinBlocks -> lane; batches
+    // of <= kLatencyMaxBlocks blocks of any size -> pipelined; blocks of
+    // <= kSmallOut bytes in batches of <= kSmallMaxBlocks -> LDS form;
+    // everything else -> one wave per block.
     static const char* env = getenv("LZ4E_DECOMPRESS_MODE");
     uint32_t mode = a.mode;
     if (mode == kDecAuto && env)
-        mode = env[0] == 'w' ? kDecWave
-                             : (env[0] == 'p' ? kDecPipe
-                                              : (env[0] == 'c' ? kDecChunk : (env[0] == 'r' ? kDecRelay : kDecAuto)));
-    if (mode == kDecAuto && env && env[0] == 's') mode = kDecSmall;
-    if (mode == kDecAuto && env && env[0] == 'l') mode = kDecLane;
+        mode = env[0] == 'w'   ? kDecWave
+               : env[0] == 'p' ? kDecPipe
+               : env[0] == 's' ? kDecSmall
+               : env[0] == 'l' ? kDecLane
+                               : kDecAuto;
     if (mode == kDecAuto)
         mode = (a.max_cap == 0 || (a.max_cap >= kPipeMinCap && a.max_cap < kPipeMaxCap))
                    ? kDecPipe
@@ -3246,42 +2212,6 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
                                  ? kDecPipe
                                  : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks <= kSmallMaxBlocks ? kDecSmall
                                                                                                      : kDecWave)));
-    if (mode == kDecRelay) {
-        const int om = launch_order_mode(false);
-        uint32_t* order = nullptr;
-        if ((om == kOrderAlways || (om == kOrderAuto && a.nblocks > 256 * ((160u * 1024u) / sizeof(RelayLds)))) &&
-            hipMallocAsync((void**)&order, sizeof(uint32_t) * a.nblocks, stream) == hipSuccess) {
-            hipLaunchKernelGGL((order_kernel<DecodeWeight>), dim3(1), dim3(kOrderThreads), 0, stream,
-                               DecodeWeight{a.src_len, a.dst_cap}, a.nblocks, order);
-        } else {
-            (void)hipGetLastError();
-            order = nullptr;
-        }
-        hipLaunchKernelGGL((decompress_relay_kernel<kStamps>), dim3(a.nblocks), dim3(2 * kWave), 0, stream,
-                           a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
-                           dbg, a.dict_len, (const uint32_t*)order);
-        const hipError_t err = hipGetLastError();
-        if (order) (void)hipFreeAsync(order, stream);
-        return err;
-    }
-    if (mode == kDecChunk) {
-        const int om = launch_order_mode(false);
-        uint32_t* order = nullptr;
-        if ((om == kOrderAlways || (om == kOrderAuto && a.nblocks > 256 * kCkPerCu)) &&
-            hipMallocAsync((void**)&order, sizeof(uint32_t) * a.nblocks, stream) == hipSuccess) {
-            hipLaunchKernelGGL((order_kernel<DecodeWeight>), dim3(1), dim3(kOrderThreads), 0, stream,
-                               DecodeWeight{a.src_len, a.dst_cap}, a.nblocks, order);
-        } else {
-            (void)hipGetLastError();
-            order = nullptr;
-        }
-        hipLaunchKernelGGL((decompress_chunk_kernel<kStamps>), dim3(a.nblocks), dim3(kWave), 0, stream,
-                           a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
-                           dbg, a.dict_len, (const uint32_t*)order);
-        const hipError_t err = hipGetLastError();
-        if (order) (void)hipFreeAsync(order, stream);
-        return err;
-    }
     if (mode == kDecPipe) {
         const int om = launch_order_mode(false);
         uint32_t* order = nullptr;

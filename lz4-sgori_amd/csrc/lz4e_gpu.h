@@ -38,20 +38,19 @@ struct DecompressBatch {
     const int32_t* dst_cap;
     int32_t* ret;
     uint32_t nblocks;
-    // Upper bound of dst_cap[] (0: unknown): blocks of 16 KiB up to 128 KiB
-    // (or unknown) take the pipelined 4-wave decoder, smaller and larger ones
-    // one wave each.
+    // Upper bound of dst_cap[] (0: unknown); with the batch size it selects
+    // the decoder (launch_impl in lz4e_decompress.hip lists the order).
     uint32_t max_cap;
-    uint32_t mode = 0;  // kDecAuto, or force kDecWave / kDecPipe / kDecChunk / kDecRelay / kDecSmall / kDecLane (tests, A/B)
+    uint32_t mode = 0;  // kDecAuto, or force kDecWave / kDecPipe / kDecSmall / kDecLane (tests, A/B)
     // Dictionary mode (nullable): block i decodes with the dict_len[i] bytes
     // right before dst + dst_off[i] as its dictionary (extDict semantics of
     // lz4e_decompress.c:299-302, 339-378; <= 64 KiB of it is ever read).
     const int32_t* dict_len = nullptr;
 };
 
-// (3 was the streaming decoder, removed in round 4: the chunked decoder
-// replaced it)
-enum : uint32_t { kDecAuto = 0, kDecWave = 1, kDecPipe = 2, kDecChunk = 4, kDecRelay = 5, kDecSmall = 6, kDecLane = 7 };
+// (3 was the streaming decoder, removed in round 4; 4 and 5 the chunked and
+// relay decoders, removed in round 5: none was ever picked by auto mode)
+enum : uint32_t { kDecAuto = 0, kDecWave = 1, kDecPipe = 2, kDecSmall = 6, kDecLane = 7 };
 
 // Launch order policy (lz4e_order.h): 0 block order, 1 heavy first when the
 // batch is large enough (default), 2 heavy first always.  From

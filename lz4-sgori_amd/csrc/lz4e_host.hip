@@ -181,6 +181,24 @@ struct Lease {
 // host + off[b], rounded up to 16 B (offsets are 16-B aligned and every slot
 // has >= 16 B of slack).  Only the bytes that exist come back over PCIe --
 // not the whole capacity -- and no DMA copy waits behind another stream's.
+// Clock probe (diagnostic): one wave spins on a dependent VALU chain for
+// `iters` steps between two pairs of time stamps, so the host can read the
+// shader clock the chip holds right now as delta s_memtime (shader cycles,
+// MI355X_MICROARCH.md:488) over delta s_memrealtime (100 MHz, :503).
+__global__ __launch_bounds__(64) void clock_probe_kernel(uint64_t* out, uint32_t iters) {
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t x = threadIdx.x;
+    for (uint32_t i = 0; i < iters; ++i) x = x * 1664525u + 1013904223u;
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        out[0] = t1 - t0;
+        out[1] = r1 - r0;
+        out[2] = x;  // keeps the chain
+    }
+}
+
 __global__ __launch_bounds__(256) void copy_blocks_kernel(const uint8_t* __restrict__ dev,
                                                           uint8_t* __restrict__ host,
                                                           const uint64_t* __restrict__ off,
@@ -562,6 +580,24 @@ int lz4e_compress_sg_batch(struct lz4e_sg_request* reqs, int n) {
     return compress_sg_batch_impl(reqs, n, nullptr, nullptr);
 }
 
+// One coalesced batch of single compress calls.  A batch that fails as a
+// whole (staging, launch) is bisected, so that one caller's failure is not
+// everyone's and a single bad request costs O(log n) reruns, not n.
+static void run_compress_calls(CompressCall** batch, size_t n) {
+    std::vector<lz4e_sg_request> reqs(n);
+    for (size_t i = 0; i < n; ++i) reqs[i] = batch[i]->q;
+    const int r = compress_sg_batch_impl(reqs.data(), (int)n, nullptr, nullptr);
+    if (r < 0 && n > 1) {
+        run_compress_calls(batch, n / 2);
+        run_compress_calls(batch + n / 2, n - n / 2);
+        return;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        batch[i]->q.ret = r < 0 ? 0 : reqs[i].ret;
+        batch[i]->err = g_err;
+    }
+}
+
 int LZ4E_compress_default(const struct bio_vec* src, struct bio_vec* dst, struct bvec_iter* srcIter,
                           struct bvec_iter* dstIter, void* wrkmem) {
     if (wrkmem) std::memset(wrkmem, 0, LZ4E_MEM_COMPRESS);  // lz4e_compress.c:548
@@ -572,23 +608,7 @@ int LZ4E_compress_default(const struct bio_vec* src, struct bio_vec* dst, struct
         &call,
         [](CompressCall** batch, size_t n) {
             maybe_inject_fault();
-            std::vector<lz4e_sg_request> reqs(n);
-            for (size_t i = 0; i < n; ++i) reqs[i] = batch[i]->q;
-            int r = compress_sg_batch_impl(reqs.data(), (int)n, nullptr, nullptr);
-            if (r < 0 && n > 1) {
-                // the batch as a whole failed (staging, launch): each call
-                // alone, so that one caller's failure is not everyone's
-                for (size_t i = 0; i < n; ++i) {
-                    const int ri = compress_sg_batch_impl(&reqs[i], 1, nullptr, nullptr);
-                    batch[i]->q.ret = ri < 0 ? 0 : reqs[i].ret;
-                    batch[i]->err = g_err;
-                }
-                return;
-            }
-            for (size_t i = 0; i < n; ++i) {
-                batch[i]->q.ret = r < 0 ? 0 : reqs[i].ret;
-                batch[i]->err = g_err;
-            }
+            run_compress_calls(batch, n);
         },
         [](CompressCall* c, const std::string& why) {
             c->q.ret = 0;
@@ -624,7 +644,15 @@ uint64_t decode_staging(int csize, int cap) {
     return std::min<uint64_t>((uint64_t)cap, most);
 }
 
-void lz4e_debug_coalescer_fault(int k) { g_coalescer_faults.store(k < 0 ? 0 : k); }
+// Test hook, armed only when LZ4E_TEST_FAULTS=1 is in the environment (a
+// production caller cannot make the single calls fail through it): returns 0
+// when armed, -1 when refused.
+int lz4e_debug_coalescer_fault(int k) {
+    const char* e = getenv("LZ4E_TEST_FAULTS");
+    if (!e || strcmp(e, "1") != 0) return -1;
+    g_coalescer_faults.store(k < 0 ? 0 : k);
+    return 0;
+}
 
 }  // extern "C"
 
@@ -718,42 +746,41 @@ int lz4e_decompress_batch(const char* const* src, const int* csize, char* const*
     return decompress_batch_impl(src, csize, dst, cap, ret, n, nullptr, nullptr);
 }
 
+// One coalesced batch of single decompress calls; a batch that fails as a
+// whole (staging, launch, a watchdog on some block) is bisected, so that
+// only the caller whose block failed sees the failure.
+static void run_decompress_calls(DecompressCall** batch, size_t n) {
+    std::vector<const char*> src(n);
+    std::vector<char*> dst(n);
+    std::vector<int> cs(n), cap(n), ret(n, -1);
+    for (size_t i = 0; i < n; ++i) {
+        src[i] = batch[i]->src;
+        dst[i] = batch[i]->dst;
+        cs[i] = batch[i]->csize;
+        cap[i] = batch[i]->cap;
+    }
+    const int r = decompress_batch_impl(src.data(), cs.data(), dst.data(), cap.data(), ret.data(), (int)n,
+                                        nullptr, nullptr);
+    if (r < 0 && n > 1) {
+        run_decompress_calls(batch, n / 2);
+        run_decompress_calls(batch + n / 2, n - n / 2);
+        return;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        // a failed call: the block's own value if it has one (the
+        // watchdog's LZ4E_DECODE_ABORTED), else -1
+        batch[i]->ret = r < 0 ? (ret[i] < 0 ? ret[i] : -1) : ret[i];
+        batch[i]->err = g_err;
+    }
+}
+
 int LZ4E_decompress_safe(const char* source, char* dest, int compressedSize, int maxDecompressedSize) {
     DecompressCall call{source, dest, compressedSize, maxDecompressedSize};
     decompress_calls().submit(
         &call,
         [](DecompressCall** batch, size_t n) {
             maybe_inject_fault();
-            std::vector<const char*> src(n);
-            std::vector<char*> dst(n);
-            std::vector<int> cs(n), cap(n), ret(n, -1);
-            for (size_t i = 0; i < n; ++i) {
-                src[i] = batch[i]->src;
-                dst[i] = batch[i]->dst;
-                cs[i] = batch[i]->csize;
-                cap[i] = batch[i]->cap;
-            }
-            const int r = decompress_batch_impl(src.data(), cs.data(), dst.data(), cap.data(), ret.data(),
-                                                (int)n, nullptr, nullptr);
-            if (r < 0 && n > 1) {
-                // the batch failed as a whole (staging, launch, a watchdog
-                // on some block): each call alone, so that only the caller
-                // whose block failed sees the failure
-                for (size_t i = 0; i < n; ++i) {
-                    int ri = -1;
-                    const int g = decompress_batch_impl(&src[i], &cs[i], &dst[i], &cap[i], &ri, 1, nullptr,
-                                                        nullptr);
-                    batch[i]->ret = g < 0 ? (ri < 0 ? ri : -1) : ri;
-                    batch[i]->err = g_err;
-                }
-                return;
-            }
-            for (size_t i = 0; i < n; ++i) {
-                // a failed call: the block's own value if it has one (the
-                // watchdog's LZ4E_DECODE_ABORTED), else -1
-                batch[i]->ret = r < 0 ? (ret[i] < 0 ? ret[i] : -1) : ret[i];
-                batch[i]->err = g_err;
-            }
+            run_decompress_calls(batch, n);
         },
         [](DecompressCall* c, const std::string& why) {
             c->ret = -1;
@@ -837,8 +864,15 @@ int lz4e_debug_compress_stamped(const uint8_t* src, const uint64_t* src_off, con
                : -1;
 }
 
+// Diagnostic (not part of include/lz4e.h): clock_probe_kernel on `stream`
+// (out: 3 x u64 in device memory: delta s_memtime, delta s_memrealtime, junk).
+int lz4e_debug_clock_probe(void* stream, uint64_t* out, uint32_t iters) {
+    hipLaunchKernelGGL(clock_probe_kernel, dim3(1), dim3(64), 0, static_cast<hipStream_t>(stream), out, iters);
+    return hip_ok(hipGetLastError(), "clock probe launch") ? 0 : -1;
+}
+
 // Diagnostic (not part of include/lz4e.h): the decompress kernels with a
-// forced decoder (mode 0 auto, 1 one wave per block, 2 pipelined, 3 streaming)
+// forced decoder (mode 0 auto, 1 one wave per block, 2 pipelined, 6 LDS form, 7 lane)
 // and, when dbg is not null, the stamped build's per-block cycle counters
 // (one-wave decoder: 8 x u64 per block; pipelined and streaming: 20 x u64,
 // tools/decab.py, tools/streamab.py; dbg zeroed by the caller).
@@ -846,6 +880,9 @@ int lz4e_debug_decompress_stamped(const uint8_t* src, const uint64_t* src_off, c
                                   uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
                                   int32_t* ret, uint32_t nblocks, void* stream, uint64_t* dbg,
                                   uint32_t max_cap, uint32_t mode) {
+    if (mode != lz4e::kDecAuto && mode != lz4e::kDecWave && mode != lz4e::kDecPipe && mode != lz4e::kDecSmall &&
+        mode != lz4e::kDecLane)
+        return -1;
     lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap, mode};
     const hipStream_t s = static_cast<hipStream_t>(stream);
     return hip_ok(dbg ? lz4e::launch_decompress_stamped(a, s, dbg) : lz4e::launch_decompress(a, s),

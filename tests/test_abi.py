@@ -135,9 +135,12 @@ def test_coalescer_unwinds_a_throwing_batch(amd):
 
     L = amd.lib()
     L.lz4e_debug_coalescer_fault.argtypes = [ctypes.c_int]
-    L.lz4e_debug_coalescer_fault.restype = None
+    L.lz4e_debug_coalescer_fault.restype = ctypes.c_int
     L.lz4e_last_error.restype = ctypes.c_char_p
-    L.lz4e_debug_coalescer_fault(1 << 20)
+    os.environ.pop("LZ4E_TEST_FAULTS", None)
+    assert L.lz4e_debug_coalescer_fault(1) == -1  # refused unless armed by the environment
+    os.environ["LZ4E_TEST_FAULTS"] = "1"
+    assert L.lz4e_debug_coalescer_fault(1 << 20) == 0
     results = []
 
     def caller(k):
@@ -161,6 +164,7 @@ def test_coalescer_unwinds_a_throwing_batch(amd):
         assert not any(t.is_alive() for t in ts), "a caller of a throwing batch never returned"
     finally:
         L.lz4e_debug_coalescer_fault(0)
+        os.environ.pop("LZ4E_TEST_FAULTS", None)
     assert len(results) == 64
     assert all(r < 0 and "injected fault" in e for r, e in results), results[:4]
     # the coalescer still serves calls

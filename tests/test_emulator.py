@@ -143,12 +143,10 @@ def _emu_decode(exe, tmp_path, frame, cap, dic=b"", flag="-d"):
 DEC_CASES = [(k, m) for k in ("text", "records", "runs", "small_alpha") for m in range(5)]
 
 
-# the chunked decoder (mode 4, never auto-picked) on a subset
-DEC_RUNS = [(k, m, "-d") for k, m in DEC_CASES] + [(k, m, "-c") for k, m in DEC_CASES if k in ("text", "runs")]
+DEC_RUNS = [(k, m, "-d") for k, m in DEC_CASES]
 
 
-@pytest.mark.parametrize("kind,mode,flag", DEC_RUNS,
-                         ids=[f"{k}-{m}-{'wave' if f == '-d' else 'chunk'}" for k, m, f in DEC_RUNS])
+@pytest.mark.parametrize("kind,mode,flag", DEC_RUNS, ids=[f"{k}-{m}-wave" for k, m, f in DEC_RUNS])
 def test_emulated_decoder_sanitized(emu_exe, tmp_path, kind, mode, flag):
     """Valid frames (mode 0), truncations (1), bit flips (2), short capacity
     (3) and a dictionary (4; with a shortened dictionary on odd seeds): the
@@ -333,18 +331,13 @@ def _emu_decode_pipe(exe, tmp_path, frame, cap, dic=b"", flag="-p"):
 PIPE_CASES = [(k, m) for k in ("text", "records", "ints", "runs") for m in range(5)] + [("random", 0)]
 
 
-# the chunked and relay decoders (modes 4 and 5, never auto-picked) on a subset
-PIPE_RUNS = [(k, m, "-p") for k, m in PIPE_CASES] + \
-    [(k, m, f) for k, m in PIPE_CASES if k == "text" for f in ("-c", "-r")]
-_PN = {"-p": "pipe", "-c": "chunk", "-r": "relay"}
+PIPE_RUNS = [(k, m, "-p") for k, m in PIPE_CASES]
+_PN = {"-p": "pipe"}
 
 
 @pytest.mark.parametrize("kind,mode,flag", PIPE_RUNS, ids=[f"{k}-{m}-{_PN[f]}" for k, m, f in PIPE_RUNS])
 def test_emulated_pipe_decoder_sanitized(emu_exe, tmp_path, kind, mode, flag):
-    """The 4-wave pipelined decoder (-p), the one-wave chunked decoder (-c:
-    speculative token walks, LDS output window, HBM far sources) and the
-    2-wave relay decoder (-r: parser wave + sequence copier wave)
-    on 16-64 KiB blocks: valid frames (mode 0), truncations (1), bit flips
+    """The 4-wave pipelined decoder (-p) on 16-64 KiB blocks: valid frames (mode 0), truncations (1), bit flips
     (2), short capacity (3) and a dictionary (4): values, error codes and
     bytes equal the oracle's (/root/reference/lz4e/lz4e_decompress.c:62-460
     restated)."""
@@ -379,7 +372,7 @@ def emu_exe_spin1(tmp_path_factory):
     shutil.rmtree(b, ignore_errors=True)
 
 
-@pytest.mark.parametrize("flag", ["-p", "-r"], ids=["pipe", "relay"])
+@pytest.mark.parametrize("flag", ["-p"], ids=["pipe"])
 def test_emulated_pipe_decoder_watchdog(emu_exe_spin1, tmp_path, flag):
     """A forced watchdog: every wave leaves its loop (the run ends), the
     block's value is LZ4E_DECODE_ABORTED -- even though the parser itself

@@ -72,7 +72,7 @@ def _gpu_compress(amd, blocks, ttypes, caps=None):
     return r, frames, ax
 
 
-DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_CHUNK, DEC_RELAY, DEC_SMALL, DEC_LANE = 0, 1, 2, 4, 5, 6, 7
+DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_SMALL, DEC_LANE = 0, 1, 2, 6, 7
 
 
 def _gpu_decompress(amd, frames, caps, csizes=None, max_cap=None, mode=DEC_AUTO):
@@ -276,8 +276,8 @@ def test_decompress_batch_vs_oracle(gpu, kind):
         assert outs[i] == eo == expect[i]
 
 
-@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_CHUNK, DEC_RELAY, DEC_PIPE, DEC_WAVE, DEC_SMALL, DEC_LANE],
-                         ids=["auto", "chunk", "relay", "pipe", "wave", "small", "lane"])
+@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_PIPE, DEC_WAVE, DEC_SMALL, DEC_LANE],
+                         ids=["auto", "pipe", "wave", "small", "lane"])
 @pytest.mark.parametrize("mode", ["truncate", "flip", "garbage", "small_cap", "csize"])
 def test_decompress_error_codes(gpu, mode, dec):
     rng = np.random.default_rng(1234 + len(mode))
@@ -378,7 +378,7 @@ def test_full_size_roundtrip(gpu, cls, bs, kind):
         assert frames[i] == oracle_ref.compress(blocks[i], cls)[1]
 
 
-@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_CHUNK, DEC_RELAY], ids=["wave", "pipe", "chunk", "relay"])
+@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE], ids=["wave", "pipe"])
 def test_decompress_huge_runs(gpu, mode):
     """Blocks whose sequences are hundreds of MiB long: a 256 MiB run of one
     byte (a single match whose length extension is ~1 MiB of 0xFF) and a
@@ -397,7 +397,7 @@ def test_decompress_huge_runs(gpu, mode):
         assert outs[i] == b, i
 
 
-@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_CHUNK, DEC_RELAY], ids=["wave", "pipe", "chunk", "relay"])
+@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE], ids=["wave", "pipe"])
 @pytest.mark.parametrize("cap_extra", [0, 100000])
 def test_decompress_periodic_matches(gpu, cap_extra, mode):
     """Self-overlapping matches of every period 1..40 and lengths around
@@ -744,8 +744,7 @@ def test_full_size_sg512_layout_every_frame(gpu):
 @pytest.mark.parametrize("kind", ["mixed", "text", "runs", "ints", "random", "small_alpha", "fio"])
 def test_decompress_pipelined_vs_wave_decoder(gpu, kind):
     """The four decoders on the same frames -- the pipelined 4-wave decoder,
-    the relay decoder, the one-wave chunked decoder and the one-wave decoder
-    -- valid frames,
+    the one-wave decoder, its LDS form and the lane decoder -- valid frames,
     exact and spare capacities, and corrupted ones: identical values and
     bytes, all equal to the oracle's."""
     rng = np.random.default_rng(zlib.crc32(kind.encode()))
@@ -774,15 +773,13 @@ def test_decompress_pipelined_vs_wave_decoder(gpu, kind):
         want.append(oracle_ref.decompress(f, cap))
     r_wg, o_wg = _gpu_decompress(gpu, frames, caps, mode=DEC_PIPE)
     r_wv, o_wv = _gpu_decompress(gpu, frames, caps, mode=DEC_WAVE)
-    r_ck, o_ck = _gpu_decompress(gpu, frames, caps, mode=DEC_CHUNK)
-    r_rl, o_rl = _gpu_decompress(gpu, frames, caps, mode=DEC_RELAY)
     r_sm, o_sm = _gpu_decompress(gpu, frames, caps, mode=DEC_SMALL)
     r_ln, o_ln = _gpu_decompress(gpu, frames, caps, mode=DEC_LANE)
     for i, (er, eb) in enumerate(want):
-        assert r_wg[i] == er == r_wv[i] == r_ck[i] == r_rl[i] == r_sm[i] == r_ln[i], \
-            (i, r_wg[i], er, r_wv[i], r_ck[i], r_rl[i], r_sm[i], r_ln[i])
+        assert r_wg[i] == er == r_wv[i] == r_sm[i] == r_ln[i], \
+            (i, r_wg[i], er, r_wv[i], r_sm[i], r_ln[i])
         if er >= 0:
-            assert o_wg[i] == eb == o_wv[i] == o_ck[i] == o_rl[i] == o_sm[i] == o_ln[i], i
+            assert o_wg[i] == eb == o_wv[i] == o_sm[i] == o_ln[i], i
 
 
 # ---------------------------------------------------------------------------

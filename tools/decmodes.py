@@ -21,7 +21,7 @@ L = lz4e_amd.lib()
 P = ctypes.c_void_p
 L.lz4e_debug_decompress_stamped.argtypes = [P] * 7 + [ctypes.c_uint32, P, P, ctypes.c_uint32,
                                                        ctypes.c_uint32]
-NAMES = {1: "one-wave", 2: "pipelined", 4: "chunked", 5: "relay", 6: "lds-small", 7: "lane"}
+NAMES = {1: "one-wave", 2: "pipelined", 6: "lds-small", 7: "lane"}
 
 
 def class_blocks(kind, n, bs):

@@ -3,10 +3,6 @@
 //   emu_main -d FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (one-wave decoder)
 //   emu_main -p FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (pipelined decoder,
 //            4 waves: parser + 3 copiers)
-//   emu_main -c FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (chunked decoder,
-//            one wave)
-//   emu_main -r FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (relay decoder,
-//            2 waves: parser + sequence copier)
 //   emu_main -l FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (one-wave decoder,
 //            LDS output for blocks of <= 4608 bytes without a dictionary)
 //   emu_main -n FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (lane-per-block
@@ -65,9 +61,9 @@ static int decode_main(int argc, char** argv) {
     // the decoder reads the input window by aligned dwords (the GPU's word
     // granularity: the dword holding the last byte); the heap block covers it
     frame.reserve((frame.size() + 3) & ~(size_t)3);
-    // kDecPipe / kDecChunk / kDecRelay / kDecSmall / kDecWave
+    // kDecPipe / kDecSmall / kDecLane / kDecWave
     const char m = argv[1][1];
-    const uint32_t mode = m == 'p' ? 2u : (m == 'c' ? 4u : (m == 'r' ? 5u : (m == 'l' ? 6u : (m == 'n' ? 7u : 1u))));
+    const uint32_t mode = m == 'p' ? 2u : (m == 'l' ? 6u : (m == 'n' ? 7u : 1u));
     emu_decompress_batch_mode(frame.data(), &so, &csize, out.data(), &doff, &cap, &ret, 1, &D, mode);
     char err[256];
     const int good = emu_decode_results(&ret, 1, err, sizeof err);
@@ -83,8 +79,7 @@ static int decode_main(int argc, char** argv) {
 
 int main(int argc, char** argv) {
     if (argc > 3 && argv[1][0] == '-' &&
-        (argv[1][1] == 'd' || argv[1][1] == 'p' || argv[1][1] == 'c' || argv[1][1] == 'r' ||
-         argv[1][1] == 'l' || argv[1][1] == 'n'))
+        (argv[1][1] == 'd' || argv[1][1] == 'p' || argv[1][1] == 'l' || argv[1][1] == 'n'))
         return decode_main(argc, argv);
     if (argc < 3) {
         fprintf(stderr, "usage: emu_main BLOCK_FILE TABLE_CLASS [FRAME_OUT]\n");
