@@ -1,0 +1,1119 @@
+// lz4e_band.hip -- gfx950 band-parallel LZ4E compressor (round 5).
+//
+// Restates LZ4E_compress_generic (/root/reference/lz4e/lz4e_compress.c:218-534,
+// noDict, acceleration 1) bit-exactly with one 256-thread workgroup per
+// block and no wave-serial walk over the block's positions.
+//
+// The greedy parse is a pure function of the candidate every lookup sees, and
+// that candidate is "the latest put of the same hash before the lookup"
+// (puts: every probe :329-330, the match end - 2 :461-463, the rematch
+// position :484; an empty slot reads as position 0, :548 + :150-166).  The
+// workgroup works on a band of kB positions ahead of the verified frontier f,
+// in passes ("Band compressor"):
+//
+//  1. candidates: under a guess G of the put set, a position's candidate is
+//     the nearest G-marked position on its full-population same-hash chain
+//     inside [f, p) (prev_kernel precomputes the chain links), else the true
+//     table T (every committed put before f);
+//  2. verify: each lookup the previous pass's chain made whose outcome (miss,
+//     or hit and its candidate) is unchanged under the new candidates is what
+//     the reference does: every lookup before the first changed one saw
+//     exactly the puts its own parse made before it, so that prefix IS the
+//     reference's parse;
+//  3. commit the prefix: emit its sequences, write its puts to T, move f;
+//  4. hits, match lengths (capped at kFCap) and catch-up lengths of the
+//     positions whose candidate changed;
+//  5. next(e) for every band position e: where the parse goes when a match
+//     ends at e (rematch at e :467-493, else the step-1 search from e + 1,
+//     :292-336, to its first hit);
+//  6. the chain from the frontier's state through the band: pointer doubling
+//     inside 64-position segments (one per wave slot, ds_bpermute), then a
+//     stitch over the 16 segments;
+//  7. the chain's own puts are the next pass's guess G.
+//
+// Searches past their 66th probe (skip steps >= 2) only ever start a pass
+// (the entry search): its probes are evaluated in parallel over the closed-
+// form schedule.  A match longer than kFCap ends a pass and is extended
+// exactly by the whole workgroup.  Limited output (:358-363, :425-430,
+// :505-509) is checked per sequence before its bytes are written.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "lz4e_device.h"
+#include "lz4e_gpu.h"
+
+namespace lz4e {
+
+namespace {
+
+constexpr uint32_t kB = 1024;         // band width (positions)
+constexpr uint32_t kBT = 256;         // threads per workgroup (4 waves)
+constexpr uint32_t kBS = kB / kBT;    // band slots per thread
+constexpr uint32_t kSegs = kB / 64;   // 64-position segments (one per wave slot)
+constexpr uint32_t kFCap = 32;        // match bytes compared per position (more: "long")
+constexpr uint32_t kBCap = 16;        // catch-up bytes compared per position
+constexpr uint32_t kFLong = 0xFFFFu;  // fwd field of a long match
+constexpr uint32_t kHops = 4;         // direct chain hops before pointer jumping
+constexpr uint32_t kNone = 0xFFFFu;
+constexpr uint32_t kEntry = 0xFFFu;   // code value: the entry search (no node)
+constexpr uint32_t kLongLits = 8;     // long literal runs copied by the workgroup per commit
+
+// next codes (u16): kind << 12 | value (a band offset, or kEntry)
+enum : uint32_t {
+    kNode = 0,      // value: band offset of the next node (a match end)
+    kExitRem = 1,   // value: the node; its match ends at or past the band end
+    kExitSrch = 2,  // value: the node; its step-1 search runs past the band end
+    kSlow = 3,      // value: the node; 66 probes, no hit: the search goes on sparse
+    kEndLim = 4,    // value: the node; its search reaches mflimit: last literals
+    kLong = 5,      // value: the node; its match is longer than kFCap
+    kEndRem = 6,    // value: the node itself lies past mflimit: last literals
+};
+LZ4E_DEV uint32_t code(uint32_t kind, uint32_t v) { return kind << 12 | v; }
+LZ4E_DEV uint32_t ckind(uint32_t c) { return c >> 12; }
+LZ4E_DEV uint32_t cval(uint32_t c) { return c & 0xFFFu; }
+
+// position flags (gf): what the last chain did at a position
+enum : uint32_t {
+    kFLook = 1,  // looked up
+    kFRem = 2,   // ... as a rematch (else as a search probe)
+    kFHit = 4,   // ... and found a match
+    kFNode = 8,  // a match of the chain ends here (a chain node)
+    kFKill = 16, // commit: a later put of the same hash exists
+};
+
+// parse states
+enum : uint32_t { kStRem = 0, kStSrch = 1, kStEnd = 2 };
+
+// uniform state slots
+enum : uint32_t {
+    sF = 0,                      // band start (the verified frontier)
+    sEK, sEP, sEJ, sEA,          // entry state: kind, position, probe index, anchor
+    sHave,                       // a chain exists for this band start
+    sTK, sTP, sTJ, sTA, sTF,     // that chain's end state (+ final position of an end)
+    sLQ, sLF,                    // its long match: hit position, exact length (sLQ kNone-ish: none)
+    sOp,                         // output bytes emitted
+    sFill,                       // the ring holds positions [.., sFill)
+    sDone, sFail,
+    sTerm,                       // the chain's terminal code
+    sE0,                         // the chain's first code
+    sNLong,                      // long literal runs of this commit
+    sBadA,                       // commit: anchor offset + 1 of the first changed lookup
+    sTotal,                      // commit: bytes of its sequences
+    sFinal,                      // the end state's final source position
+    kStN
+};
+
+struct BandLds {
+    // the true table at the frontier: byU16 8192 x u16, byU32 4096 x u32,
+    // byU64 2048 x u32 (lz4e_compress.c:48-57)
+    uint32_t T[4096];
+    // per band position (ring index p & (kB - 1)):
+    uint32_t ph[kB];   // prev delta (bits 0-15, 0: none), hash (16-28), G (31)
+    uint32_t hi[kB];   // hit (bit 0), valid (bit 1), back (8-15), fwd (16-31, kFLong)
+    uint16_t cd[kB];   // candidate delta hi[] was computed for (0: none)
+    uint16_t nx[kB];   // scratch: ancestor links, segment exit codes
+    uint8_t gf[kB];    // flags of the last chain (kF*)
+    uint64_t hmask[kSegs];        // hit positions per segment
+    uint32_t segv[kSegs];         // block scan scratch
+    uint32_t hfirst[kSegs + 1];   // first hit offset at or after each segment start
+    uint16_t entry[kSegs];        // chain entry lane per segment (kNone: none)
+    uint32_t red[4];
+    uint32_t st[kStN];
+    uint32_t lng[3 * kLongLits];  // long literal runs: source, length, output position
+};
+
+struct Img {
+    ByteBuf b;
+    LZ4E_DEV uint32_t rd32(uint32_t q) const { return buf_ld32(b, q); }
+    LZ4E_DEV uint32_t rd8(uint32_t q) const { return buf_ld8(b, q); }
+};
+
+template <int TT>
+LZ4E_DEV uint32_t hash_at(const Img& im, uint32_t p) {
+    if (TT == kByU32) {
+        const uint64_t v = (uint64_t)im.rd32(p) | ((uint64_t)im.rd32(p + 4) << 32);
+        return hash5(v, 12);
+    }
+    return hash4(im.rd32(p), TT == kByU64 ? 11u : 13u);
+}
+
+// ---- wave / block helpers ---------------------------------------------------
+
+// Inclusive scan over the 64 lanes (DPP row shifts and row broadcasts).
+template <class Op>
+LZ4E_DEV uint32_t wave_scan(uint32_t v, Op op, uint32_t id) {
+    const uint32_t lane = lane_id();
+    uint32_t x = v, t;
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x111, 0xf, 0xf, false);
+    x = (lane & 15) >= 1 ? op(x, t) : x;
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x112, 0xf, 0xf, false);
+    x = (lane & 15) >= 2 ? op(x, t) : x;
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x114, 0xf, 0xf, false);
+    x = (lane & 15) >= 4 ? op(x, t) : x;
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x118, 0xf, 0xf, false);
+    x = (lane & 15) >= 8 ? op(x, t) : x;
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x142, 0xa, 0xf, false);
+    x = (lane & 16) ? op(x, t) : x;
+    t = (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)x, 0x143, 0xc, 0xf, false);
+    x = (lane & 32) ? op(x, t) : x;
+    return x;
+}
+
+struct OpMax {
+    LZ4E_DEV uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
+};
+struct OpMin {
+    LZ4E_DEV uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; }
+};
+struct OpAdd {
+    LZ4E_DEV uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
+};
+
+// ---- per-position match data ------------------------------------------------
+
+// Forward match length of p against c from p + 4 (lz4e_compress.c:420-423),
+// bytes below matchlimit, capped: kFLong when kFCap bytes all matched and
+// more remain.
+LZ4E_DEV uint32_t fwd_len(const Img& im, uint32_t p, uint32_t c, uint32_t matchlimit) {
+    if (p + 4 >= matchlimit) return 0;
+    const uint32_t lim = matchlimit - (p + 4);
+    uint32_t a[kFCap / 4], b[kFCap / 4];
+#pragma unroll
+    for (uint32_t i = 0; i < kFCap / 4; ++i) {
+        a[i] = im.rd32(p + 4 + 4 * i);
+        b[i] = im.rd32(c + 4 + 4 * i);
+    }
+    uint32_t n = kFCap;
+#pragma unroll
+    for (int i = kFCap / 4 - 1; i >= 0; --i) {
+        const uint32_t x = a[i] ^ b[i];
+        if (x) n = 4 * (uint32_t)i + ((uint32_t)__builtin_ctz(x) >> 3);
+    }
+    if (n >= lim) return lim;
+    return n >= kFCap ? kFLong : n;
+}
+
+// Catch-up length of p against c (:339-349) without the anchor limit: equal
+// bytes right below both while c - i > 0, capped at kBCap.
+LZ4E_DEV uint32_t back_len(const Img& im, uint32_t p, uint32_t c) {
+    uint32_t lim = c < kBCap ? c : kBCap;
+    if (lim == 0) return 0;
+    // the 4 bytes right below x - 4 i, top-aligned (below position 0: zeros,
+    // never counted: lim <= c <= p)
+    auto below = [&](uint32_t x, uint32_t i) -> uint32_t {
+        const uint32_t q = 4 * i + 4;
+        if (x >= q) return im.rd32(x - q);
+        if (x > 4 * i) return im.rd32(0) << (8 * (q - x));
+        return 0u;
+    };
+    uint32_t n = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < kBCap / 4; ++i) {
+        const uint32_t x = below(p, i) ^ below(c, i);
+        if (n == 4 * i) n += x ? ((uint32_t)__builtin_clz(x) >> 3) : 4u;
+    }
+    return n < lim ? n : lim;
+}
+
+// The reference's catch-up loop, for a capped one that saturated.
+LZ4E_DEV uint32_t back_exact(const Img& im, uint32_t p, uint32_t c, uint32_t lim) {
+    uint32_t i = 0;
+    while (i < lim && c - i > 0 && im.rd8(p - 1 - i) == im.rd8(c - 1 - i)) ++i;
+    return i;
+}
+
+// ---- the pre-kernel: full-population same-hash links ---------------------------
+
+// pd[p] = p - q for the latest q < p with hash(q) == hash(p) and p - q <=
+// 65535, else 0, for p <= mflimit.  One wave per block walks the block in
+// 64-position chunks: a lane's predecessor inside its chunk comes from one
+// ballot per hash bit, otherwise from the table of latest positions (read
+// before this chunk's writes; each hash written by its group's last lane).
+template <int TT>
+LZ4E_DEV void prev_block(const Img& im, uint32_t n, uint16_t* __restrict__ pd, uint32_t* last) {
+    const uint32_t lane = lane_id();
+    const uint32_t hlog = TT == kByU64 ? 11u : (TT == kByU32 ? 12u : 13u);
+    for (uint32_t i = lane; i < (1u << hlog); i += 64) last[i] = 0;
+    lockstep();
+    const uint32_t mflimit = n - kMfLimit;
+    const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+    for (uint32_t base = 0; base <= mflimit; base += 64) {
+        const uint32_t p = base + lane;
+        const bool on = p <= mflimit;
+        const uint32_t h = on ? hash_at<TT>(im, p) : (1u << hlog) + lane;  // off lanes: unique keys
+        uint64_t m = ~0ull;
+        for (uint32_t k = 0; k <= hlog + 6; ++k) {
+            const bool bit = (h >> k) & 1;
+            const uint64_t bb = ballot(bit);
+            m &= bit ? bb : ~bb;
+        }
+        const uint64_t lower = m & below;
+        const uint32_t prev_in = on ? last[h] : 0u;  // latest earlier chunk's position + 1
+        lockstep();
+        const bool group_last = ((m >> lane) >> 1) == 0;
+        if (on && group_last) last[h] = p + 1;
+        lockstep();
+        uint32_t d = 0;
+        if (lower) d = lane - (63 - (uint32_t)__builtin_clzll(lower));
+        else if (prev_in && p - (prev_in - 1) <= kMaxDistance) d = p - (prev_in - 1);
+        if (on) pd[p] = (uint16_t)d;
+    }
+}
+
+__global__ __launch_bounds__(64) void prev_kernel(const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+                                                  const uint32_t* __restrict__ src_len,
+                                                  const uint8_t* __restrict__ table_type, uint16_t* __restrict__ pdbuf,
+                                                  uint32_t max_len) {
+    __shared__ uint32_t last[8192];
+    const uint32_t b = blockIdx.x;
+    const uint32_t n = src_len[b];
+    if (n < kMinLength || n > max_len) return;
+    const Img im{buf_make(src + src_off[b], n)};
+    uint16_t* pd = pdbuf + (size_t)b * max_len;
+    const int tt = table_type[b];
+    if (tt == kByU32) prev_block<kByU32>(im, n, pd, last);
+    else if (tt == kByU64) prev_block<kByU64>(im, n, pd, last);
+    else prev_block<kByU16>(im, n, pd, last);
+}
+
+// ---- the band kernel ----------------------------------------------------------
+
+template <int TT>
+struct Band {
+    BandLds& S;
+    Img im;
+    uint32_t n, mflimit, matchlimit, cap;
+    bool limited;
+    uint8_t* out;
+    const uint16_t* pd;
+    uint32_t t, w, lane;
+
+    LZ4E_DEV static uint32_t slot(uint32_t p) { return p & (kB - 1); }
+    LZ4E_DEV uint32_t F() const { return S.st[sF]; }
+    // ring index of band offset o (hi, cd, gf persist across passes)
+    LZ4E_DEV uint32_t rg(uint32_t o) const { return (S.st[sF] + o) & (kB - 1); }
+
+    LZ4E_DEV uint32_t tget(uint32_t h) const {
+        if (TT == kByU16) return ((const uint16_t*)S.T)[h];
+        return S.T[h];
+    }
+    LZ4E_DEV void tput(uint32_t h, uint32_t p) const {
+        if (TT == kByU16) ((uint16_t*)S.T)[h] = (uint16_t)p;
+        else S.T[h] = p;
+    }
+
+    // ---- block reductions / scans ----
+    template <class Op>
+    LZ4E_DEV uint32_t block_reduce(uint32_t v, Op op, uint32_t id) {
+        uint32_t m = wave_scan(v, op, id);
+        m = lane_val(m, 63);
+        if (lane == 0) S.red[w] = m;
+        block_sync();
+        const uint32_t r = op(op(S.red[0], S.red[1]), op(S.red[2], S.red[3]));
+        block_sync();
+        return r;
+    }
+    LZ4E_DEV uint32_t block_any(bool v) {
+        const uint32_t m = ballot(v) != 0;
+        if (lane == 0) S.red[w] = m;
+        block_sync();
+        const uint32_t r = S.red[0] | S.red[1] | S.red[2] | S.red[3];
+        block_sync();
+        return r;
+    }
+    // Inclusive scan over the band in position order (slot s of thread t is
+    // band offset 256 s + t: segment 4 s + wave, lane = place in it);
+    // returns the total.
+    template <class Op>
+    LZ4E_DEV uint32_t band_scan(uint32_t (&v)[kBS], Op op, uint32_t id) {
+        uint32_t x[kBS];
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            x[s] = wave_scan(v[s], op, id);
+            const uint32_t tot = lane_val(x[s], 63);
+            if (lane == 0) S.segv[4 * s + w] = tot;
+        }
+        block_sync();
+        uint32_t acc = id, all = id;
+        for (uint32_t k = 0; k < kSegs; ++k) {
+            const uint32_t sv = S.segv[k];
+#pragma unroll
+            for (uint32_t s = 0; s < kBS; ++s)
+                if (k == 4 * s + w) v[s] = op(acc, x[s]);
+            acc = op(acc, sv);
+            all = acc;
+        }
+        block_sync();
+        return all;
+    }
+
+    // ---- ring fill: positions [max(sFill, f), f + kB) ----
+    LZ4E_DEV void fill() {
+        const uint32_t f = F();
+        const uint32_t from = S.st[sFill] > f ? S.st[sFill] : f, to = f + kB;
+        block_sync();
+        for (uint32_t p = from + t; p < to; p += kBT) {
+            const uint32_t o = slot(p);
+            if (p <= mflimit) {
+                const uint32_t h = hash_at<TT>(im, p);
+                S.ph[o] = (uint32_t)pd[p] | (h << 16) | 0x80000000u;  // G = 1: the first guess
+            } else {
+                S.ph[o] = 0;
+            }
+            S.hi[o] = 0;
+            S.cd[o] = 0;
+            S.gf[o] = 0;
+        }
+        if (t == 0) S.st[sFill] = to;
+        block_sync();
+    }
+
+    // ---- 1. candidates of my positions under G: delta (0: none / too far) ----
+    LZ4E_DEV uint32_t from_table(uint32_t p, uint32_t e) const {
+        const uint32_t q = tget((e >> 16) & 0x1FFFu);
+        return p - q <= kMaxDistance ? p - q : 0u;
+    }
+    LZ4E_DEV void cands(uint32_t (&cdl)[kBS]) {
+        const uint32_t f = F();
+        uint32_t pend = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t, p = f + o;
+            cdl[s] = 0;
+            if (p > mflimit) continue;
+            const uint32_t e = S.ph[slot(p)];
+            uint32_t c = o, d = e & 0xFFFFu;
+            uint32_t how = 2;  // 0 resolved in band, 1 table, 2 pending
+            for (uint32_t k = 0; k < kHops; ++k) {
+                if (d == 0 || d > c) {
+                    how = 1;
+                    break;
+                }
+                c -= d;
+                const uint32_t ec = S.ph[slot(f + c)];
+                if (ec >> 31) {
+                    how = 0;
+                    break;
+                }
+                d = ec & 0xFFFFu;
+            }
+            if (how == 0) cdl[s] = o - c;
+            else if (how == 1) cdl[s] = from_table(p, e);
+            else pend |= 1u << s;
+        }
+        if (!block_any(pend != 0)) return;
+        // pointer jumping over every band position: nx[o] = an ancestor with
+        // only unmarked chain positions between (kNone: none in the band)
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t, p = f + o;
+            const uint32_t d = p <= mflimit ? S.ph[slot(p)] & 0xFFFFu : 0u;
+            S.nx[o] = (uint16_t)((d == 0 || d > o) ? kNone : o - d);
+        }
+        block_sync();
+        for (;;) {
+            bool more = false;
+#pragma unroll
+            for (uint32_t s = 0; s < kBS; ++s) {
+                const uint32_t o = 256 * s + t;
+                const uint32_t a = S.nx[o];
+                if (a == kNone || (S.ph[slot(f + a)] >> 31)) continue;
+                const uint32_t a2 = S.nx[a];
+                S.nx[o] = (uint16_t)a2;
+                more |= a2 != kNone;
+            }
+            block_sync();
+            if (!block_any(more)) break;
+        }
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            if (!((pend >> s) & 1)) continue;
+            const uint32_t o = 256 * s + t, p = f + o;
+            const uint32_t a = S.nx[o];
+            cdl[s] = a != kNone ? o - a : from_table(p, S.ph[slot(p)]);
+        }
+        block_sync();
+    }
+
+    LZ4E_DEV bool hit_of(uint32_t p, uint32_t d) const { return d != 0 && im.rd32(p - d) == im.rd32(p); }
+
+    // probe position of index j of the entry search (state SRCH(sEP, sEJ))
+    LZ4E_DEV uint32_t probe_pos(uint32_t j) const {
+        return S.st[sEP] + (uint32_t)(probe_offset(j) - probe_offset(S.st[sEJ]));
+    }
+
+    // ---- 2. first lookup of the last chain whose outcome differs ----
+    LZ4E_DEV uint32_t verify(const uint32_t (&cdl)[kBS]) {
+        uint32_t first = ~0u;
+        const uint32_t f = F();
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t;
+            const uint32_t g = S.gf[rg(o)];
+            if (!(g & kFLook) || cdl[s] == S.cd[rg(o)]) continue;
+            if (hit_of(f + o, cdl[s]) || (g & kFHit)) first = first < o ? first : o;
+        }
+        return block_reduce(first, OpMin(), ~0u);
+    }
+
+    // ---- 3. commit ----
+    struct Seq {
+        uint32_t lit, ll, off, ml;
+    };
+    // the sequence found by the lookup at band offset o, anchor a
+    LZ4E_DEV Seq seq_at(uint32_t o, uint32_t a) const {
+        const uint32_t x = F() + o;
+        const uint32_t g = S.gf[rg(o)], h = S.hi[rg(o)], d = S.cd[rg(o)];
+        uint32_t fw = h >> 16;
+        if (fw == kFLong) fw = S.st[sLF];  // the chain's long match (sLQ == x)
+        Seq q;
+        q.off = d;
+        if (g & kFRem) {
+            q.lit = x;
+            q.ll = 0;
+            q.ml = 4 + fw;
+        } else {
+            uint32_t bk = (h >> 8) & 0xFFu;
+            const uint32_t lim = x - a;
+            if (bk >= kBCap && lim > kBCap) bk = back_exact(im, x, x - d, lim);
+            if (bk > lim) bk = lim;
+            q.lit = a;
+            q.ll = x - bk - a;
+            q.ml = 4 + fw + bk;
+        }
+        return q;
+    }
+    LZ4E_DEV static uint32_t seq_size(const Seq& q) {
+        uint32_t sz = 1 + q.ll + 2;
+        if (q.ll >= 15) sz += 1 + (q.ll - 15) / 255;
+        if (q.ml - 4 >= 15) sz += 1 + (q.ml - 4 - 15) / 255;
+        return sz;
+    }
+    // the reference's output checks of a limited call (:358-363, :425-430)
+    LZ4E_DEV bool seq_fits(const Seq& q, uint32_t op) const {
+        const uint64_t o1 = (uint64_t)op + 1;
+        if (o1 + q.ll + 8 + q.ll / 255 > cap) return false;
+        uint64_t o2 = o1 + q.ll + 2;
+        if (q.ll >= 15) o2 += 1 + (q.ll - 15) / 255;
+        return o2 + 6 + ((q.ml - 4) >> 8) <= cap;
+    }
+    LZ4E_DEV void put8(uint32_t q, uint32_t v) const { out[q] = (uint8_t)v; }
+    // token and literal-length varint; returns the literals' position
+    LZ4E_DEV uint32_t write_head(const Seq& q, uint32_t op) const {
+        const uint32_t mc = q.ml - 4;
+        const uint32_t tok = (q.ll >= 15 ? 0xF0u : q.ll << 4) + (mc >= 15 ? 15u : mc);
+        put8(op++, tok);
+        if (q.ll >= 15) {
+            uint32_t r = q.ll - 15;
+            for (; r >= 255; r -= 255) put8(op++, 255);
+            put8(op++, r);
+        }
+        return op;
+    }
+    LZ4E_DEV void write_tail(const Seq& q, uint32_t op) const {
+        put8(op++, q.off & 0xFFu);
+        put8(op++, q.off >> 8);
+        const uint32_t mc = q.ml - 4;
+        if (mc >= 15) {
+            uint32_t r = mc - 15;
+            for (; r >= 255; r -= 255) put8(op++, 255);
+            put8(op++, r);
+        }
+    }
+    LZ4E_DEV void copy_lits(uint32_t dst, uint32_t src, uint32_t len) const {
+        for (uint32_t i = 0; i < len; ++i) put8(dst + i, im.rd8(src + i));
+    }
+    LZ4E_DEV void copy_lits_wg(uint32_t dst, uint32_t src, uint32_t len) const {
+        for (uint32_t i = t; i < len; i += kBT) put8(dst + i, im.rd8(src + i));
+    }
+
+    // Commits the last chain's lookups before band offset `bad` (~0: all,
+    // up to the chain's end state): sequences, puts to T, the new state.
+    LZ4E_DEV void commit(uint32_t bad, const uint32_t (&cdl)[kBS]) {
+        const uint32_t f = F();
+        const uint32_t ea = S.st[sEA];
+        // latest node at or before each position (offset + 1; 0: none)
+        uint32_t an[kBS];
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t;
+            an[s] = (S.gf[rg(o)] & kFNode) ? o + 1 : 0u;
+        }
+        band_scan(an, OpMax(), 0u);
+        // sequences of the verified finding lookups
+        Seq sq[kBS];
+        uint32_t sz[kBS], ex[kBS];
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t;
+            const uint32_t g = S.gf[rg(o)];
+            sz[s] = 0;
+            if (bad != ~0u && o == bad) S.st[sBadA] = (g & kFNode) ? 0u : an[s];
+            if (o < bad && (g & kFLook) && (g & kFHit)) {
+                // a probe is never a node, so its latest node is before it
+                const uint32_t a = an[s] ? f + an[s] - 1 : ea;
+                sq[s] = seq_at(o, a);
+                sz[s] = seq_size(sq[s]);
+            }
+            ex[s] = sz[s];
+        }
+        const uint32_t total = band_scan(ex, OpAdd(), 0u);  // (its barriers publish sBadA)
+        const uint32_t op0 = S.st[sOp];
+        bool bad_fit = false;
+        if (limited) {
+#pragma unroll
+            for (uint32_t s = 0; s < kBS; ++s)
+                if (sz[s] && !seq_fits(sq[s], op0 + ex[s] - sz[s])) bad_fit = true;
+        }
+        if (block_any(bad_fit)) {
+            if (t == 0) {
+                S.st[sFail] = 1;
+                S.st[sDone] = 1;
+            }
+            block_sync();
+            return;
+        }
+        if (t == 0) S.st[sNLong] = 0;
+        block_sync();
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            if (!sz[s]) continue;
+            const uint32_t lo = write_head(sq[s], op0 + ex[s] - sz[s]);
+            bool own = sq[s].ll <= 64;
+            if (!own) {
+                const uint32_t k = atomicAdd(&S.st[sNLong], 1u);
+                if (k < kLongLits) {
+                    S.lng[3 * k] = sq[s].lit;
+                    S.lng[3 * k + 1] = sq[s].ll;
+                    S.lng[3 * k + 2] = lo;
+                } else {
+                    own = true;
+                }
+            }
+            if (own) copy_lits(lo, sq[s].lit, sq[s].ll);
+            write_tail(sq[s], lo + sq[s].ll);
+        }
+        block_sync();
+        {
+            const uint32_t nl = S.st[sNLong] < kLongLits ? S.st[sNLong] : kLongLits;
+            for (uint32_t k = 0; k < nl; ++k) copy_lits_wg(S.lng[3 * k + 2], S.lng[3 * k], S.lng[3 * k + 1]);
+        }
+        // the new state (uniform)
+        uint32_t nk, np, nj, na, nfin = 0;
+        if (bad == ~0u) {
+            nk = S.st[sTK];
+            np = S.st[sTP];
+            nj = S.st[sTJ];
+            na = S.st[sTA];
+            nfin = S.st[sTF];
+        } else {
+            const uint32_t x = f + bad;
+            const uint32_t g = S.gf[rg(bad)];
+            np = x;
+            if (g & kFRem) {
+                nk = kStRem;
+                nj = 0;
+                na = x;
+            } else {
+                nk = kStSrch;
+                const uint32_t ba = S.st[sBadA];
+                if (ba) {
+                    na = f + ba - 1;
+                    nj = x - (na + 1);
+                } else {
+                    // a probe of the entry search: its index
+                    na = ea;
+                    uint32_t lo = S.st[sEJ], hi = lo + kB;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (probe_pos(mid) < x) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    nj = lo;
+                }
+            }
+        }
+        // T: the puts below the new frontier (kill each put's previous put of
+        // its hash; the survivors are the last of theirs)
+        const uint32_t nf = nk == kStEnd ? f + kB : np;
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t, p = f + o;
+            if (p >= nf || p > mflimit || !(S.ph[slot(p)] >> 31)) continue;
+            const uint32_t d = cdl[s];
+            if (d && d <= o) S.gf[rg(o - d)] |= kFKill;
+        }
+        block_sync();
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t, p = f + o;
+            if (p >= nf || p > mflimit) continue;
+            const uint32_t e = S.ph[slot(p)];
+            if ((e >> 31) && !(S.gf[rg(o)] & kFKill)) tput((e >> 16) & 0x1FFFu, p);
+        }
+        block_sync();
+        if (t == 0) {
+            // a match end past the band: its put(e - 2) (:461-463)
+            if (nk == kStRem && np <= mflimit && np - 2 >= f + kB) tput(hash_at<TT>(im, np - 2), np - 2);
+            S.st[sOp] = op0 + total;
+            S.st[sEK] = nk;
+            S.st[sEP] = np;
+            S.st[sEJ] = nj;
+            S.st[sEA] = na;
+            S.st[sFinal] = nfin;
+            S.st[sHave] = 0;
+            S.st[sLQ] = ~0u;
+            if (nk == kStEnd) S.st[sDone] = 1;
+            else S.st[sF] = np;
+        }
+        block_sync();
+    }
+
+    // ---- 4. hits and match lengths of the positions whose candidate changed ----
+    LZ4E_DEV void hits(const uint32_t (&cdl)[kBS]) {
+        const uint32_t f = F();
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t, p = f + o;
+            if (p > mflimit) continue;
+            const uint32_t d = cdl[s];
+            if ((S.hi[rg(o)] & 2) && S.cd[rg(o)] == d) continue;
+            uint32_t h = 2;
+            if (hit_of(p, d)) {
+                const uint32_t c = p - d;
+                h |= 1u | (back_len(im, p, c) << 8) | (fwd_len(im, p, c, matchlimit) << 16);
+            }
+            S.hi[rg(o)] = h;
+            S.cd[rg(o)] = (uint16_t)d;
+        }
+        block_sync();
+    }
+
+    // first hit at band offset >= y (kNone: none in the band)
+    LZ4E_DEV uint32_t nh(uint32_t y) const {
+        if (y >= kB) return kNone;
+        const uint32_t k = y >> 6;
+        const uint64_t m = S.hmask[k] >> (y & 63);
+        return m ? y + ctz64(m) : S.hfirst[k + 1];
+    }
+    // last probe of the step-1 search from s (probes s, s+1, ..., each
+    // passing its end check :301-302; probe 65 advances by 2); below s: none
+    LZ4E_DEV uint32_t qmax_of(uint32_t s) const {
+        if (s + 65 + 2 <= mflimit) return s + 65;
+        const uint32_t a = s + 64, b = mflimit - 1;
+        return a < b ? a : b;
+    }
+
+    // ---- 5. next code of band offset o ----
+    LZ4E_DEV uint32_t next_code(uint32_t o) const {
+        const uint32_t f = F(), e = f + o;
+        if (e > mflimit) return code(kEndRem, o);
+        uint32_t q;  // band offset of the hit
+        const uint32_t h = S.hi[rg(o)];
+        if (h & 1) {
+            q = o;  // rematch (:484-493)
+        } else {
+            const uint32_t s = e + 1, qm = qmax_of(s);
+            const uint32_t y = nh(o + 1);
+            if (y == kNone || f + y > qm) {
+                if (qm < f + kB || qm < s) return (s + 65 + 2 <= mflimit) ? code(kSlow, o) : code(kEndLim, o);
+                return code(kExitSrch, o);
+            }
+            q = y;
+        }
+        const uint32_t fw = S.hi[rg(q)] >> 16;
+        if (fw == kFLong) return code(kLong, o);
+        const uint32_t end = q + 4 + fw;
+        return end < kB ? code(kNode, end) : code(kExitRem, o);
+    }
+
+    // Exact match length from q + 4 against q - d + 4 (the whole workgroup).
+    LZ4E_DEV uint32_t fwd_exact(uint32_t q, uint32_t d) {
+        const uint32_t c = q - d, lim = q + 4 < matchlimit ? matchlimit - (q + 4) : 0u;
+        for (uint32_t i = 0; i < lim; i += 4 * kBT) {
+            const uint32_t k = i + 4 * t;
+            uint32_t m = ~0u;
+            if (k < lim) {
+                uint32_t x = im.rd32(q + 4 + k) ^ im.rd32(c + 4 + k);
+                if (lim - k < 4) x &= (1u << (8 * (lim - k))) - 1u;
+                if (x) m = k + ((uint32_t)__builtin_ctz(x) >> 3);
+            }
+            const uint32_t r = block_reduce(m, OpMin(), ~0u);
+            if (r != ~0u) return r;
+        }
+        return lim;
+    }
+
+    // ---- 6-7. the chain from the entry state; flags and the next guess ----
+    LZ4E_DEV void chain() {
+        const uint32_t f = F();
+        // hit masks per segment
+        uint32_t hb[kBS];
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t;
+            hb[s] = (f + o <= mflimit) && (S.hi[rg(o)] & 1);
+            const uint64_t m = ballot(hb[s] != 0);
+            if (lane == 0) S.hmask[4 * s + w] = m;
+        }
+        block_sync();
+        if (t == 0) {
+            uint32_t nxt = kNone;
+            S.hfirst[kSegs] = kNone;
+            for (int k = kSegs - 1; k >= 0; --k) {
+                if (S.hmask[k]) nxt = 64 * (uint32_t)k + ctz64(S.hmask[k]);
+                S.hfirst[k] = nxt;
+            }
+        }
+        // the entry state's first event (uniform)
+        const uint32_t ek = S.st[sEK];
+        block_sync();
+        uint32_t e0;
+        uint32_t jE = ~0u, jX = ~0u, qE = 0;  // entry search: first event / exit probe index
+        bool eEnd = false;
+        if (ek == kStRem) {
+            e0 = code(kNode, 0);
+        } else {
+            const uint32_t j0 = S.st[sEJ];
+            uint32_t ev = ~0u, exi = ~0u;
+            for (uint32_t r = 0; r < kBS; ++r) {
+                const uint32_t j = j0 + t + kBT * r, x = probe_pos(j);
+                if (x >= f + kB) {
+                    exi = exi < j ? exi : j;
+                    continue;
+                }
+                if (x + probe_step(j) > mflimit || (S.hi[rg(x - f)] & 1)) ev = ev < j ? ev : j;
+            }
+            jE = block_reduce(ev, OpMin(), ~0u);
+            jX = block_reduce(exi, OpMin(), ~0u);
+            if (jE < jX) {
+                const uint32_t x = probe_pos(jE);
+                if (x + probe_step(jE) > mflimit) {
+                    eEnd = true;
+                    e0 = code(kEndLim, kEntry);
+                } else {
+                    qE = x - f;
+                    const uint32_t fw = S.hi[rg(qE)] >> 16;
+                    if (fw == kFLong) e0 = code(kLong, kEntry);
+                    else {
+                        const uint32_t end = qE + 4 + fw;
+                        e0 = end < kB ? code(kNode, end) : code(kExitRem, kEntry);
+                    }
+                }
+            } else {
+                e0 = code(kExitSrch, kEntry);
+            }
+        }
+        // in-segment pointer doubling: J (next lane, 64: left the segment),
+        // M (lanes visited), X (the exit code)
+        uint32_t Mlo[kBS], Mhi[kBS];
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t;
+            const uint32_t c = next_code(o);
+            uint32_t J = (ckind(c) == kNode && (cval(c) >> 6) == (o >> 6)) ? cval(c) & 63u : 64u;
+            uint32_t X = c;
+            Mlo[s] = lane < 32 ? 1u << lane : 0u;
+            Mhi[s] = lane >= 32 ? 1u << (lane - 32) : 0u;
+#pragma unroll
+            for (uint32_t r = 0; r < 6; ++r) {
+                const uint32_t src = J < 64 ? J : lane;
+                const uint32_t Jn = shfl(J, src), Xn = shfl(X, src);
+                const uint32_t Ln = shfl(Mlo[s], src), Hn = shfl(Mhi[s], src);
+                if (J < 64) {
+                    J = Jn;
+                    X = Xn;
+                    Mlo[s] |= Ln;
+                    Mhi[s] |= Hn;
+                }
+            }
+            S.nx[o] = (uint16_t)X;
+        }
+        block_sync();
+        if (t == 0) {
+            for (uint32_t k = 0; k < kSegs; ++k) S.entry[k] = (uint16_t)kNone;
+            uint32_t cur = e0;
+            while (ckind(cur) == kNode) {
+                const uint32_t o = cval(cur);
+                S.entry[o >> 6] = (uint16_t)(o & 63);
+                cur = S.nx[o];
+            }
+            S.st[sTerm] = cur;
+        }
+        block_sync();
+        const uint32_t term = S.st[sTerm];
+        // node flags of my positions
+        uint32_t node[kBS];
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t k = 4 * s + w, en = S.entry[k];
+            uint32_t bit = 0;
+            if (en != kNone) {
+                const uint32_t ml = lane_val(Mlo[s], en), mh = lane_val(Mhi[s], en);
+                bit = lane < 32 ? (ml >> lane) & 1u : (mh >> (lane - 32)) & 1u;
+            }
+            node[s] = bit;
+        }
+        // the terminal: the end state (uniform)
+        const uint32_t tk = ckind(term), tv = cval(term);
+        uint32_t TK = kStEnd, TP = 0, TJ = 0, TA = 0, TF = 0, LQ = ~0u, LF = 0;
+        {
+            // the hit of the terminal's node (or of the entry search)
+            uint32_t q = kNone;
+            if (tv == kEntry) q = qE;
+            else if (tk == kExitRem || tk == kLong) q = (S.hi[rg(tv)] & 1) ? tv : nh(tv + 1);
+            if (tk == kEndRem) {
+                TK = kStEnd;
+                TF = f + tv;
+                TA = f + tv;
+            } else if (tk == kEndLim) {
+                TK = kStEnd;
+                if (tv == kEntry) {
+                    TF = jE == 0 ? f : probe_pos(jE) - probe_step(jE - 1);
+                    TA = S.st[sEA];
+                } else {
+                    const uint32_t s0 = f + tv + 1, qm = qmax_of(s0);
+                    TF = qm >= s0 ? qm : s0;
+                    TA = f + tv;
+                }
+            } else if (tk == kExitSrch) {
+                TK = kStSrch;
+                if (tv == kEntry) {
+                    TP = probe_pos(jX);
+                    TJ = jX;
+                    TA = S.st[sEA];
+                } else {
+                    TP = f + kB;
+                    TJ = f + kB - (f + tv + 1);
+                    TA = f + tv;
+                }
+            } else if (tk == kSlow) {
+                TK = kStSrch;
+                TP = f + tv + 68;
+                TJ = 66;
+                TA = f + tv;
+            } else {  // kExitRem, kLong
+                uint32_t fw = S.hi[rg(q)] >> 16;
+                if (tk == kLong) {
+                    fw = fwd_exact(f + q, S.cd[rg(q)]);
+                    LQ = f + q;
+                    LF = fw;
+                }
+                const uint32_t end = f + q + 4 + fw;
+                TK = kStRem;
+                TP = end;
+                TA = end;
+                if (end > mflimit) {
+                    TK = kStEnd;
+                    TF = end;
+                }
+            }
+        }
+        // the end state's position: flags below it, G kept at and above it
+        const uint32_t tpo = TK == kStEnd ? kB : (TP - f < kB ? TP - f : kB);
+        // node flags to LDS (puts at e - 2 read the neighbours')
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t;
+            S.gf[rg(o)] = node[s] ? (uint8_t)kFNode : (uint8_t)0;
+        }
+        // probes of the nodes' searches: latest node at or before each position
+        uint32_t an[kBS];
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) an[s] = node[s] ? 256 * s + t + 1 : 0u;
+        band_scan(an, OpMax(), 0u);  // (barriers: gf node flags published)
+        uint32_t jlo = 0, jhi = 0;  // entry search probes [jlo, jhi] looked up
+        bool ehit = false;
+        if (ek == kStSrch) {
+            jlo = S.st[sEJ];
+            const uint32_t jl = jE < jX ? jE : jX;
+            jhi = jl;  // exclusive unless the event is a hit
+            ehit = jE < jX && !eEnd;
+            if (ehit) jhi = jE + 1;
+        }
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t, p = f + o;
+            uint32_t g = 0;
+            bool put = false;
+            if (o < tpo && p <= mflimit) {
+                const uint32_t h = S.hi[rg(o)];
+                if (node[s]) {
+                    g = kFNode | kFLook | kFRem | ((h & 1) ? kFHit : 0u);
+                    put = true;
+                } else if (an[s]) {
+                    const uint32_t v = an[s] - 1;  // the latest node, before o
+                    if (f + v <= mflimit && !(S.hi[rg(v)] & 1)) {
+                        const uint32_t s0 = f + v + 1, qm = qmax_of(s0);
+                        const uint32_t y = nh(v + 1);
+                        const uint32_t lim = (y != kNone && f + y <= qm) ? f + y : qm;
+                        if (p <= lim && qm >= s0) {
+                            g = kFLook | ((h & 1) ? kFHit : 0u);
+                            put = true;
+                        }
+                    }
+                }
+                if (o + 2 < kB && (S.gf[rg(o + 2)] & kFNode) && p + 2 <= mflimit) put = true;
+                if (TK == kStRem && p + 2 == TP) put = true;
+            } else if (node[s]) {
+                g = kFNode;  // a node past mflimit (the end) or at the end state
+            }
+            g |= (uint32_t)(S.gf[rg(o)] & kFNode);
+            if (o < tpo) {
+                const uint32_t e = S.ph[slot(p)];
+                S.ph[slot(p)] = (e & 0x7FFFFFFFu) | (put ? 0x80000000u : 0u);
+            }
+            S.gf[rg(o)] = (uint8_t)g;
+        }
+        block_sync();
+        // the entry search's probes (band offsets from the schedule)
+        if (ek == kStSrch) {
+            for (uint32_t r = 0; r < kBS; ++r) {
+                const uint32_t j = jlo + t + kBT * r;
+                if (j >= jhi) continue;
+                const uint32_t x = probe_pos(j);
+                if (x >= f + kB) continue;
+                const uint32_t o = x - f;
+                S.gf[rg(o)] = (uint8_t)(kFLook | ((S.hi[rg(o)] & 1) ? kFHit : 0u));
+                S.ph[slot(x)] |= 0x80000000u;
+            }
+        }
+        block_sync();
+        if (t == 0) {
+            S.st[sTK] = TK;
+            S.st[sTP] = TP;
+            S.st[sTJ] = TJ;
+            S.st[sTA] = TA;
+            S.st[sTF] = TF;
+            S.st[sLQ] = LQ;
+            S.st[sLF] = LF;
+            S.st[sHave] = 1;
+        }
+        block_sync();
+    }
+};
+
+template <int TT>
+LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, uint32_t cap, const uint16_t* pd,
+                         int32_t* ret, uint32_t* aux) {
+    const uint32_t t = threadIdx.x;
+    Band<TT> B{S, im, n, n >= kMinLength ? n - kMfLimit : 0u, n >= kMinLength ? n - kLastLiterals : 0u, cap,
+               cap < (uint32_t)(n + n / 255 + 16), out, pd, t, t >> 6, t & 63};
+    for (uint32_t i = t; i < 4096; i += kBT) S.T[i] = 0;  // :548 (an empty slot reads as position 0)
+    if (t == 0) {
+        for (uint32_t i = 0; i < kStN; ++i) S.st[i] = 0;
+        S.st[sF] = 1;
+        S.st[sEK] = kStSrch;  // :280-282: put(0) (== the empty slot), search from 1
+        S.st[sEP] = 1;
+        S.st[sEJ] = 0;
+        S.st[sEA] = 0;
+        S.st[sFill] = 1;
+        S.st[sLQ] = ~0u;
+    }
+    block_sync();
+    if (n >= kMinLength) {
+        // every commit moves the frontier by at least one position, so a
+        // block takes at most 2 n passes; more is a broken invariant, and the
+        // block fails (ret 0) instead of spinning
+        for (uint32_t pass = 0;; ++pass) {
+            if (pass > 2 * n + 64) {
+                if (t == 0) S.st[sFail] = 1;
+                block_sync();
+                break;
+            }
+            B.fill();
+            uint32_t cdl[kBS];
+            B.cands(cdl);
+            if (S.st[sHave]) {
+                const uint32_t bad = B.verify(cdl);
+                B.commit(bad, cdl);
+                if (S.st[sDone]) break;
+                continue;
+            }
+            B.hits(cdl);
+            B.chain();
+        }
+    }
+    // last literals (:500-530)
+    if (S.st[sFail]) {
+        if (t == 0) ret[0] = 0;
+        return;
+    }
+    const uint32_t anchor = n >= kMinLength ? S.st[sEA] : 0u;
+    const uint32_t R = n - anchor, op = S.st[sOp];
+    if (B.limited && (uint64_t)op + R + 1 + (R + 240) / 255 > cap) {
+        if (t == 0) ret[0] = 0;
+        return;
+    }
+    uint32_t lo = op + 1;
+    if (R >= 15) lo += 1 + (R - 15) / 255;
+    if (t == 0) {
+        uint32_t q = op;
+        if (R >= 15) {
+            uint32_t r = R - 15;
+            B.put8(q++, 0xF0);
+            for (; r >= 255; r -= 255) B.put8(q++, 255);
+            B.put8(q++, r);
+        } else {
+            B.put8(q++, R << 4);
+        }
+    }
+    B.copy_lits_wg(lo, anchor, R);
+    if (t == 0) {
+        ret[0] = (int32_t)(lo + R);
+        if (aux) {
+            aux[0] = n >= kMinLength ? S.st[sFinal] : 0u;
+            aux[1] = R;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBT) void band_kernel(const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+                                                   const uint32_t* __restrict__ src_len,
+                                                   const uint8_t* __restrict__ table_type, uint8_t* __restrict__ dst,
+                                                   const uint64_t* __restrict__ dst_off,
+                                                   const uint32_t* __restrict__ dst_cap, int32_t* __restrict__ ret,
+                                                   uint32_t* __restrict__ aux, uint32_t max_len,
+                                                   const uint16_t* __restrict__ pdbuf,
+                                                   const uint32_t* __restrict__ order) {
+    __shared__ BandLds S;
+    const uint32_t b = order ? order[blockIdx.x] : blockIdx.x;
+    const uint32_t n = src_len[b];
+    if (n > max_len) {
+        if (threadIdx.x == 0) ret[b] = 0;
+        return;
+    }
+    const Img im{buf_make(src + src_off[b], n)};
+    uint8_t* out = dst + dst_off[b];
+    const uint16_t* pd = pdbuf + (size_t)b * max_len;
+    uint32_t* ax = aux ? aux + 2 * (size_t)b : nullptr;
+    const int tt = table_type[b];
+    if (tt == kByU32) band_block<kByU32>(S, im, n, out, dst_cap[b], pd, ret + b, ax);
+    else if (tt == kByU64) band_block<kByU64>(S, im, n, out, dst_cap[b], pd, ret + b, ax);
+    else band_block<kByU16>(S, im, n, out, dst_cap[b], pd, ret + b, ax);
+}
+
+}  // namespace
+
+// The band compressor for a batch (no dictionary): prev_kernel, then
+// band_kernel in `order` (nullable).  pd scratch: 2 * max_len bytes per block.
+hipError_t launch_compress_band(const CompressBatch& a, hipStream_t stream, const uint32_t* order) {
+    if (a.nblocks == 0) return hipSuccess;
+    uint16_t* pd = nullptr;
+    const size_t bytes = 2 * (size_t)a.max_len * a.nblocks + 64;
+    hipError_t err = hipMallocAsync((void**)&pd, bytes, stream);
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(prev_kernel, dim3(a.nblocks), dim3(64), 0, stream, a.src, a.src_off, a.src_len, a.table_type, pd,
+                       a.max_len);
+    err = hipGetLastError();
+    if (err == hipSuccess) {
+        hipLaunchKernelGGL(band_kernel, dim3(a.nblocks), dim3(kBT), 0, stream, a.src, a.src_off, a.src_len,
+                           a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret, a.aux, a.max_len, pd, order);
+        err = hipGetLastError();
+    }
+    (void)hipFreeAsync(pd, stream);
+    return err;
+}
+
+}  // namespace lz4e
