@@ -58,6 +58,20 @@ constexpr uint32_t kHops = 4;         // direct chain hops before pointer jumpin
 constexpr uint32_t kNone = 0xFFFFu;
 constexpr uint32_t kEntry = 0xFFFu;   // code value: the entry search (no node)
 constexpr uint32_t kLongLits = 8;     // long literal runs copied by the workgroup per commit
+constexpr uint32_t kRing = 2048;      // byte ring: the block's bytes around the band
+constexpr uint32_t kRingPad = 64;     // mirror of ring bytes [0, 64): reads of <= 64 bytes never wrap
+
+// LDS access types (unaligned dword reads of the byte ring; every width may
+// alias every other)
+typedef __attribute__((address_space(3))) uint8_t lu8;
+typedef uint32_t __attribute__((aligned(1), may_alias)) u32a1;
+typedef __attribute__((address_space(3))) u32a1 lu32a1;
+typedef __attribute__((address_space(3), may_alias)) uint32_t lu32;
+// waves per SIMD the register allocation must allow (LDS allows 5 workgroups
+// of 4 waves per CU)
+#ifndef LZ4E_BAND_WAVES
+#define LZ4E_BAND_WAVES 4
+#endif
 
 // next codes (u16): kind << 12 | value (a band offset, or kEntry)
 enum : uint32_t {
@@ -101,6 +115,7 @@ enum : uint32_t {
     sBadA,                       // commit: anchor offset + 1 of the first changed lookup
     sTotal,                      // commit: bytes of its sequences
     sFinal,                      // the end state's final source position
+    sBFill,                      // the byte ring holds positions [.., sBFill)
     kStN
 };
 
@@ -113,6 +128,7 @@ struct BandLds {
     uint32_t hi[kB];   // hit (bit 0), valid (bit 1), back (8-15), fwd (16-31, kFLong)
     uint16_t cd[kB];   // candidate delta hi[] was computed for (0: none)
     uint16_t nx[kB];   // scratch: ancestor links, segment exit codes
+    uint16_t cn[kB];   // candidate delta under the current G (stable across a commit)
     uint8_t gf[kB];    // flags of the last chain (kF*)
     uint64_t hmask[kSegs];        // hit positions per segment
     uint32_t segv[kSegs];         // block scan scratch
@@ -121,6 +137,7 @@ struct BandLds {
     uint32_t red[4];
     uint32_t st[kStN];
     uint32_t lng[3 * kLongLits];  // long literal runs: source, length, output position
+    uint8_t by[kRing + kRingPad] __attribute__((aligned(16)));  // block byte p at p & (kRing - 1)
 };
 
 struct Img {
@@ -294,6 +311,14 @@ struct Band {
     // ring index of band offset o (hi, cd, gf persist across passes)
     LZ4E_DEV uint32_t rg(uint32_t o) const { return (S.st[sF] + o) & (kB - 1); }
 
+    // block bytes p .. p + 3 from the byte ring (p in [sBFill - kRing + 64, sBFill - 4])
+    LZ4E_DEV uint32_t rb32(uint32_t p) const { return *(const lu32a1*)((const lu8*)S.by + (p & (kRing - 1))); }
+    LZ4E_DEV uint32_t rb8(uint32_t p) const { return ((const lu8*)S.by)[p & (kRing - 1)]; }
+    LZ4E_DEV uint32_t ring_hash(uint32_t p) const {
+        if (TT == kByU32) return hash5((uint64_t)rb32(p) | ((uint64_t)rb32(p + 4) << 32), 12);
+        return hash4(rb32(p), TT == kByU64 ? 11u : 13u);
+    }
+
     LZ4E_DEV uint32_t tget(uint32_t h) const {
         if (TT == kByU16) return ((const uint16_t*)S.T)[h];
         return S.T[h];
@@ -352,12 +377,33 @@ struct Band {
     LZ4E_DEV void fill() {
         const uint32_t f = F();
         const uint32_t from = S.st[sFill] > f ? S.st[sFill] : f, to = f + kB;
+        // bytes [f - 128, f + kB + 64) in the ring (aligned dwords; the bytes
+        // below f serve catch-up compares and literal copies)
+        {
+            const uint32_t lo = f >= 128 ? f - 128 : 0u;
+            const uint32_t b0 = (S.st[sBFill] > lo ? S.st[sBFill] : lo) & ~3u, b1 = (f + kB + kRingPad + 3) & ~3u;
+            block_sync();
+            for (uint32_t q = b0 + 4 * t; q < b1; q += 4 * kBT) {
+                const uint32_t v = im.rd32(q), r = q & (kRing - 1);
+                *(lu32*)((lu8*)S.by + r) = v;
+                if (r < kRingPad) *(lu32*)((lu8*)S.by + kRing + r) = v;
+            }
+            if (t == 0) S.st[sBFill] = b1;
+        }
+        uint32_t pdv[kBS];
+#pragma unroll
+        for (uint32_t k = 0; k < kBS; ++k) {
+            const uint32_t p = from + t + kBT * k;
+            pdv[k] = p < to && p <= mflimit ? pd[p] : 0u;
+        }
         block_sync();
-        for (uint32_t p = from + t; p < to; p += kBT) {
+#pragma unroll
+        for (uint32_t k = 0; k < kBS; ++k) {
+            const uint32_t p = from + t + kBT * k;
+            if (p >= to) continue;
             const uint32_t o = slot(p);
             if (p <= mflimit) {
-                const uint32_t h = hash_at<TT>(im, p);
-                S.ph[o] = (uint32_t)pd[p] | (h << 16) | 0x80000000u;  // G = 1: the first guess
+                S.ph[o] = pdv[k] | (ring_hash(p) << 16) | 0x80000000u;  // G = 1: the first guess
             } else {
                 S.ph[o] = 0;
             }
@@ -374,14 +420,22 @@ struct Band {
         const uint32_t q = tget((e >> 16) & 0x1FFFu);
         return p - q <= kMaxDistance ? p - q : 0u;
     }
-    LZ4E_DEV void cands(uint32_t (&cdl)[kBS]) {
+    // Positions below `from` keep their candidate (cn): a commit changes
+    // neither G nor, for the positions left in the band, what T and G give
+    // together; only the positions new to the band are resolved then.
+    LZ4E_DEV void cands(uint32_t (&cdl)[kBS], uint32_t from) {
         const uint32_t f = F();
-        uint32_t pend = 0;
+        uint32_t pend = 0, mine = 0;
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s) {
             const uint32_t o = 256 * s + t, p = f + o;
             cdl[s] = 0;
             if (p > mflimit) continue;
+            if (p < from) {
+                cdl[s] = S.cn[slot(p)];
+                continue;
+            }
+            mine |= 1u << s;
             const uint32_t e = S.ph[slot(p)];
             uint32_t c = o, d = e & 0xFFFFu;
             uint32_t how = 2;  // 0 resolved in band, 1 table, 2 pending
@@ -402,7 +456,13 @@ struct Band {
             else if (how == 1) cdl[s] = from_table(p, e);
             else pend |= 1u << s;
         }
-        if (!block_any(pend != 0)) return;
+        if (block_any(pend != 0)) resolve_pending(cdl, pend);
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s)
+            if ((mine >> s) & 1) S.cn[slot(f + 256 * s + t)] = (uint16_t)cdl[s];
+    }
+    LZ4E_DEV void resolve_pending(uint32_t (&cdl)[kBS], uint32_t pend) {
+        const uint32_t f = F();
         // pointer jumping over every band position: nx[o] = an ancestor with
         // only unmarked chain positions between (kNone: none in the band)
 #pragma unroll
@@ -436,7 +496,7 @@ struct Band {
         block_sync();
     }
 
-    LZ4E_DEV bool hit_of(uint32_t p, uint32_t d) const { return d != 0 && im.rd32(p - d) == im.rd32(p); }
+    LZ4E_DEV bool hit_of(uint32_t p, uint32_t d) const { return d != 0 && im.rd32(p - d) == rb32(p); }
 
     // probe position of index j of the entry search (state SRCH(sEP, sEJ))
     LZ4E_DEV uint32_t probe_pos(uint32_t j) const {
@@ -521,7 +581,11 @@ struct Band {
             put8(op++, r);
         }
     }
+    // short literal runs (<= 64 bytes, inside the byte ring) from the ring
     LZ4E_DEV void copy_lits(uint32_t dst, uint32_t src, uint32_t len) const {
+        for (uint32_t i = 0; i < len; ++i) put8(dst + i, rb8(src + i));
+    }
+    LZ4E_DEV void copy_lits_hbm(uint32_t dst, uint32_t src, uint32_t len) const {
         for (uint32_t i = 0; i < len; ++i) put8(dst + i, im.rd8(src + i));
     }
     LZ4E_DEV void copy_lits_wg(uint32_t dst, uint32_t src, uint32_t len) const {
@@ -580,7 +644,14 @@ struct Band {
         for (uint32_t s = 0; s < kBS; ++s) {
             if (!sz[s]) continue;
             const uint32_t lo = write_head(sq[s], op0 + ex[s] - sz[s]);
-            bool own = sq[s].ll <= 64;
+            // short runs starting inside the byte ring copy from it, the
+            // others from HBM (long ones by the whole workgroup below)
+            bool own = sq[s].ll <= 64 && sq[s].lit + 128 >= f;
+            if (!own && sq[s].ll <= 64) {
+                copy_lits_hbm(lo, sq[s].lit, sq[s].ll);
+                write_tail(sq[s], lo + sq[s].ll);
+                continue;
+            }
             if (!own) {
                 const uint32_t k = atomicAdd(&S.st[sNLong], 1u);
                 if (k < kLongLits) {
@@ -588,7 +659,7 @@ struct Band {
                     S.lng[3 * k + 1] = sq[s].ll;
                     S.lng[3 * k + 2] = lo;
                 } else {
-                    own = true;
+                    copy_lits_hbm(lo, sq[s].lit, sq[s].ll);
                 }
             }
             if (own) copy_lits(lo, sq[s].lit, sq[s].ll);
@@ -671,18 +742,59 @@ struct Band {
     }
 
     // ---- 4. hits and match lengths of the positions whose candidate changed ----
+    // The candidate side's bytes come from HBM (anywhere up to 64 KiB back),
+    // the position's from the byte ring; every slot's loads are issued
+    // before any of them is used.
     LZ4E_DEV void hits(const uint32_t (&cdl)[kBS]) {
         const uint32_t f = F();
+        uint32_t todo = 0;
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s) {
             const uint32_t o = 256 * s + t, p = f + o;
-            if (p > mflimit) continue;
-            const uint32_t d = cdl[s];
-            if ((S.hi[rg(o)] & 2) && S.cd[rg(o)] == d) continue;
+            if (p <= mflimit && !((S.hi[rg(o)] & 2) && S.cd[rg(o)] == cdl[s])) todo |= 1u << s;
+        }
+        uint32_t cw[kBS][1 + kFCap / 4 + kBCap / 4];
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t p = f + 256 * s + t, d = cdl[s];
+            const uint32_t c = ((todo >> s) & 1) && d ? p - d : 0u;
+            cw[s][0] = im.rd32(c);
+#pragma unroll
+            for (uint32_t i = 0; i < kFCap / 4; ++i) cw[s][1 + i] = im.rd32(c + 4 + 4 * i);
+#pragma unroll
+            for (uint32_t i = 0; i < kBCap / 4; ++i)
+                cw[s][1 + kFCap / 4 + i] = c >= 4 * i + 4 ? im.rd32(c - 4 * i - 4)
+                                           : (c > 4 * i ? im.rd32(0) << (8 * (4 * i + 4 - c)) : 0u);
+        }
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            if (!((todo >> s) & 1)) continue;
+            const uint32_t o = 256 * s + t, p = f + o, d = cdl[s];
             uint32_t h = 2;
-            if (hit_of(p, d)) {
+            if (d && cw[s][0] == rb32(p)) {
                 const uint32_t c = p - d;
-                h |= 1u | (back_len(im, p, c) << 8) | (fwd_len(im, p, c, matchlimit) << 16);
+                // forward: bytes [p + 4, matchlimit) against [c + 4, ...)
+                uint32_t fw = 0;
+                if (p + 4 < matchlimit) {
+                    const uint32_t lim = matchlimit - (p + 4);
+                    uint32_t nn = kFCap;
+#pragma unroll
+                    for (int i = kFCap / 4 - 1; i >= 0; --i) {
+                        const uint32_t x = rb32(p + 4 + 4 * (uint32_t)i) ^ cw[s][1 + i];
+                        if (x) nn = 4 * (uint32_t)i + ((uint32_t)__builtin_ctz(x) >> 3);
+                    }
+                    fw = nn >= lim ? lim : (nn >= kFCap ? kFLong : nn);
+                }
+                // backward: equal bytes right below both while c - i > 0
+                const uint32_t lim = c < kBCap ? c : kBCap;
+                uint32_t bk = 0;
+#pragma unroll
+                for (uint32_t i = 0; i < kBCap / 4; ++i) {
+                    const uint32_t x = rb32(p - 4 * i - 4) ^ cw[s][1 + kFCap / 4 + i];
+                    if (bk == 4 * i) bk += x ? ((uint32_t)__builtin_clz(x) >> 3) : 4u;
+                }
+                bk = bk < lim ? bk : lim;
+                h |= 1u | (bk << 8) | (fw << 16);
             }
             S.hi[rg(o)] = h;
             S.cd[rg(o)] = (uint16_t)d;
@@ -994,9 +1106,25 @@ struct Band {
     }
 };
 
-template <int TT>
+// Stamped build (kSt): per block, thread 0's shader cycles per phase and the
+// pass counts (dbg[0..7]: fill, cands, verify, commit, hits, chain, passes,
+// commits; lz4e_debug_compress_band, tools/bandstamps.py).
+struct BandStamps {
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t t0 = 0;
+    LZ4E_DEV void start() { t0 = clock64(); }
+    LZ4E_DEV void lap(uint32_t k) {
+        const uint64_t t1 = clock64();
+        acc[k] += t1 - t0;
+        t0 = t1;
+    }
+};
+
+template <int TT, bool kSt>
 LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, uint32_t cap, const uint16_t* pd,
-                         int32_t* ret, uint32_t* aux) {
+                         int32_t* ret, uint32_t* aux, uint64_t* dbg) {
+    BandStamps st;
+    if (kSt) st.start();
     const uint32_t t = threadIdx.x;
     Band<TT> B{S, im, n, n >= kMinLength ? n - kMfLimit : 0u, n >= kMinLength ? n - kLastLiterals : 0u, cap,
                cap < (uint32_t)(n + n / 255 + 16), out, pd, t, t >> 6, t & 63};
@@ -1009,6 +1137,7 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
         S.st[sEJ] = 0;
         S.st[sEA] = 0;
         S.st[sFill] = 1;
+        S.st[sBFill] = 0;
         S.st[sLQ] = ~0u;
     }
     block_sync();
@@ -1016,6 +1145,7 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
         // every commit moves the frontier by at least one position, so a
         // block takes at most 2 n passes; more is a broken invariant, and the
         // block fails (ret 0) instead of spinning
+        uint32_t from = 0;  // positions whose candidate is to be resolved: >= from
         for (uint32_t pass = 0;; ++pass) {
             if (pass > 2 * n + 64) {
                 if (t == 0) S.st[sFail] = 1;
@@ -1023,16 +1153,30 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
                 break;
             }
             B.fill();
+            if (kSt) st.lap(0);
             uint32_t cdl[kBS];
-            B.cands(cdl);
-            if (S.st[sHave]) {
-                const uint32_t bad = B.verify(cdl);
+            const bool have = S.st[sHave] != 0;
+            B.cands(cdl, have ? 0u : from);
+            if (kSt) st.lap(1);
+            if (have) {
+                const uint32_t bad = B.verify(cdl), f0 = B.F();
+                if (kSt) st.lap(2);
                 B.commit(bad, cdl);
+                if (kSt) {
+                    st.lap(3);
+                    st.acc[7]++;
+                }
                 if (S.st[sDone]) break;
+                from = f0 + kB;  // the positions new to the band
                 continue;
             }
             B.hits(cdl);
+            if (kSt) st.lap(4);
             B.chain();
+            if (kSt) {
+                st.lap(5);
+                st.acc[6]++;
+            }
         }
     }
     // last literals (:500-530)
@@ -1060,6 +1204,8 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
         }
     }
     B.copy_lits_wg(lo, anchor, R);
+    if (kSt && t == 0 && dbg)
+        for (uint32_t k = 0; k < 8; ++k) dbg[k] = st.acc[k];
     if (t == 0) {
         ret[0] = (int32_t)(lo + R);
         if (aux) {
@@ -1069,14 +1215,15 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
     }
 }
 
-__global__ __launch_bounds__(kBT) void band_kernel(const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
+template <bool kSt>
+__global__ __launch_bounds__(kBT, LZ4E_BAND_WAVES) void band_kernel(const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
                                                    const uint32_t* __restrict__ src_len,
                                                    const uint8_t* __restrict__ table_type, uint8_t* __restrict__ dst,
                                                    const uint64_t* __restrict__ dst_off,
                                                    const uint32_t* __restrict__ dst_cap, int32_t* __restrict__ ret,
                                                    uint32_t* __restrict__ aux, uint32_t max_len,
                                                    const uint16_t* __restrict__ pdbuf,
-                                                   const uint32_t* __restrict__ order) {
+                                                   const uint32_t* __restrict__ order, uint64_t* dbg) {
     __shared__ BandLds S;
     const uint32_t b = order ? order[blockIdx.x] : blockIdx.x;
     const uint32_t n = src_len[b];
@@ -1089,16 +1236,17 @@ __global__ __launch_bounds__(kBT) void band_kernel(const uint8_t* __restrict__ s
     const uint16_t* pd = pdbuf + (size_t)b * max_len;
     uint32_t* ax = aux ? aux + 2 * (size_t)b : nullptr;
     const int tt = table_type[b];
-    if (tt == kByU32) band_block<kByU32>(S, im, n, out, dst_cap[b], pd, ret + b, ax);
-    else if (tt == kByU64) band_block<kByU64>(S, im, n, out, dst_cap[b], pd, ret + b, ax);
-    else band_block<kByU16>(S, im, n, out, dst_cap[b], pd, ret + b, ax);
+    uint64_t* d = kSt && dbg ? dbg + 8 * (size_t)b : nullptr;
+    if (tt == kByU32) band_block<kByU32, kSt>(S, im, n, out, dst_cap[b], pd, ret + b, ax, d);
+    else if (tt == kByU64) band_block<kByU64, kSt>(S, im, n, out, dst_cap[b], pd, ret + b, ax, d);
+    else band_block<kByU16, kSt>(S, im, n, out, dst_cap[b], pd, ret + b, ax, d);
 }
 
 }  // namespace
 
 // The band compressor for a batch (no dictionary): prev_kernel, then
 // band_kernel in `order` (nullable).  pd scratch: 2 * max_len bytes per block.
-hipError_t launch_compress_band(const CompressBatch& a, hipStream_t stream, const uint32_t* order) {
+hipError_t launch_compress_band(const CompressBatch& a, hipStream_t stream, const uint32_t* order, uint64_t* dbg) {
     if (a.nblocks == 0) return hipSuccess;
     uint16_t* pd = nullptr;
     const size_t bytes = 2 * (size_t)a.max_len * a.nblocks + 64;
@@ -1108,8 +1256,13 @@ hipError_t launch_compress_band(const CompressBatch& a, hipStream_t stream, cons
                        a.max_len);
     err = hipGetLastError();
     if (err == hipSuccess) {
-        hipLaunchKernelGGL(band_kernel, dim3(a.nblocks), dim3(kBT), 0, stream, a.src, a.src_off, a.src_len,
-                           a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret, a.aux, a.max_len, pd, order);
+        if (dbg)
+            hipLaunchKernelGGL(band_kernel<true>, dim3(a.nblocks), dim3(kBT), 0, stream, a.src, a.src_off, a.src_len,
+                               a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret, a.aux, a.max_len, pd, order, dbg);
+        else
+            hipLaunchKernelGGL(band_kernel<false>, dim3(a.nblocks), dim3(kBT), 0, stream, a.src, a.src_off,
+                               a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret, a.aux, a.max_len, pd,
+                               order, nullptr);
         err = hipGetLastError();
     }
     (void)hipFreeAsync(pd, stream);

@@ -19,5 +19,5 @@ extern "C" int emu_compress_band(const uint8_t* src, const uint64_t* src_off, co
                                  const uint32_t* dst_cap, int32_t* ret, uint32_t* aux, uint32_t nblocks,
                                  uint32_t max_len) {
     lz4e::CompressBatch a{src, src_off, src_len, table_type, dst, dst_off, dst_cap, ret, aux, nblocks, max_len};
-    return lz4e::launch_compress_band(a, nullptr, nullptr) == hipSuccess ? 0 : -1;
+    return lz4e::launch_compress_band(a, nullptr, nullptr, nullptr) == hipSuccess ? 0 : -1;
 }
