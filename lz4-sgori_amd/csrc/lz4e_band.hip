@@ -305,11 +305,14 @@ struct Band {
     uint8_t* out;
     const uint16_t* pd;
     uint32_t t, w, lane;
+    // uniform parse state: every thread keeps the same copy (values from
+    // LDS read after a barrier, block reductions, or computed from them)
+    uint32_t U[kStN];
 
     LZ4E_DEV static uint32_t slot(uint32_t p) { return p & (kB - 1); }
-    LZ4E_DEV uint32_t F() const { return S.st[sF]; }
+    LZ4E_DEV uint32_t F() const { return U[sF]; }
     // ring index of band offset o (hi, cd, gf persist across passes)
-    LZ4E_DEV uint32_t rg(uint32_t o) const { return (S.st[sF] + o) & (kB - 1); }
+    LZ4E_DEV uint32_t rg(uint32_t o) const { return (U[sF] + o) & (kB - 1); }
 
     // block bytes p .. p + 3 from the byte ring (p in [sBFill - kRing + 64, sBFill - 4])
     LZ4E_DEV uint32_t rb32(uint32_t p) const { return *(const lu32a1*)((const lu8*)S.by + (p & (kRing - 1))); }
@@ -376,19 +379,19 @@ struct Band {
     // ---- ring fill: positions [max(sFill, f), f + kB) ----
     LZ4E_DEV void fill() {
         const uint32_t f = F();
-        const uint32_t from = S.st[sFill] > f ? S.st[sFill] : f, to = f + kB;
+        const uint32_t from = U[sFill] > f ? U[sFill] : f, to = f + kB;
         // bytes [f - 128, f + kB + 64) in the ring (aligned dwords; the bytes
         // below f serve catch-up compares and literal copies)
         {
             const uint32_t lo = f >= 128 ? f - 128 : 0u;
-            const uint32_t b0 = (S.st[sBFill] > lo ? S.st[sBFill] : lo) & ~3u, b1 = (f + kB + kRingPad + 3) & ~3u;
+            const uint32_t b0 = (U[sBFill] > lo ? U[sBFill] : lo) & ~3u, b1 = (f + kB + kRingPad + 3) & ~3u;
             block_sync();
             for (uint32_t q = b0 + 4 * t; q < b1; q += 4 * kBT) {
                 const uint32_t v = im.rd32(q), r = q & (kRing - 1);
                 *(lu32*)((lu8*)S.by + r) = v;
                 if (r < kRingPad) *(lu32*)((lu8*)S.by + kRing + r) = v;
             }
-            if (t == 0) S.st[sBFill] = b1;
+            U[sBFill] = b1;
         }
         uint32_t pdv[kBS];
 #pragma unroll
@@ -411,7 +414,7 @@ struct Band {
             S.cd[o] = 0;
             S.gf[o] = 0;
         }
-        if (t == 0) S.st[sFill] = to;
+        U[sFill] = to;
         block_sync();
     }
 
@@ -500,7 +503,7 @@ struct Band {
 
     // probe position of index j of the entry search (state SRCH(sEP, sEJ))
     LZ4E_DEV uint32_t probe_pos(uint32_t j) const {
-        return S.st[sEP] + (uint32_t)(probe_offset(j) - probe_offset(S.st[sEJ]));
+        return U[sEP] + (uint32_t)(probe_offset(j) - probe_offset(U[sEJ]));
     }
 
     // ---- 2. first lookup of the last chain whose outcome differs ----
@@ -526,7 +529,7 @@ struct Band {
         const uint32_t x = F() + o;
         const uint32_t g = S.gf[rg(o)], h = S.hi[rg(o)], d = S.cd[rg(o)];
         uint32_t fw = h >> 16;
-        if (fw == kFLong) fw = S.st[sLF];  // the chain's long match (sLQ == x)
+        if (fw == kFLong) fw = U[sLF];  // the chain's long match (sLQ == x)
         Seq q;
         q.off = d;
         if (g & kFRem) {
@@ -596,7 +599,7 @@ struct Band {
     // up to the chain's end state): sequences, puts to T, the new state.
     LZ4E_DEV void commit(uint32_t bad, const uint32_t (&cdl)[kBS]) {
         const uint32_t f = F();
-        const uint32_t ea = S.st[sEA];
+        const uint32_t ea = U[sEA];
         // latest node at or before each position (offset + 1; 0: none)
         uint32_t an[kBS];
 #pragma unroll
@@ -623,23 +626,18 @@ struct Band {
             ex[s] = sz[s];
         }
         const uint32_t total = band_scan(ex, OpAdd(), 0u);  // (its barriers publish sBadA)
-        const uint32_t op0 = S.st[sOp];
+        const uint32_t op0 = U[sOp];
         bool bad_fit = false;
         if (limited) {
 #pragma unroll
             for (uint32_t s = 0; s < kBS; ++s)
                 if (sz[s] && !seq_fits(sq[s], op0 + ex[s] - sz[s])) bad_fit = true;
         }
-        if (block_any(bad_fit)) {
-            if (t == 0) {
-                S.st[sFail] = 1;
-                S.st[sDone] = 1;
-            }
-            block_sync();
+        if (limited && block_any(bad_fit)) {
+            U[sFail] = 1;
+            U[sDone] = 1;
             return;
         }
-        if (t == 0) S.st[sNLong] = 0;
-        block_sync();
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s) {
             if (!sz[s]) continue;
@@ -673,11 +671,11 @@ struct Band {
         // the new state (uniform)
         uint32_t nk, np, nj, na, nfin = 0;
         if (bad == ~0u) {
-            nk = S.st[sTK];
-            np = S.st[sTP];
-            nj = S.st[sTJ];
-            na = S.st[sTA];
-            nfin = S.st[sTF];
+            nk = U[sTK];
+            np = U[sTP];
+            nj = U[sTJ];
+            na = U[sTA];
+            nfin = U[sTF];
         } else {
             const uint32_t x = f + bad;
             const uint32_t g = S.gf[rg(bad)];
@@ -695,7 +693,7 @@ struct Band {
                 } else {
                     // a probe of the entry search: its index
                     na = ea;
-                    uint32_t lo = S.st[sEJ], hi = lo + kB;
+                    uint32_t lo = U[sEJ], hi = lo + kB;
                     while (lo < hi) {
                         const uint32_t mid = (lo + hi) >> 1;
                         if (probe_pos(mid) < x) lo = mid + 1;
@@ -723,22 +721,22 @@ struct Band {
             const uint32_t e = S.ph[slot(p)];
             if ((e >> 31) && !(S.gf[rg(o)] & kFKill)) tput((e >> 16) & 0x1FFFu, p);
         }
-        block_sync();
         if (t == 0) {
             // a match end past the band: its put(e - 2) (:461-463)
             if (nk == kStRem && np <= mflimit && np - 2 >= f + kB) tput(hash_at<TT>(im, np - 2), np - 2);
-            S.st[sOp] = op0 + total;
-            S.st[sEK] = nk;
-            S.st[sEP] = np;
-            S.st[sEJ] = nj;
-            S.st[sEA] = na;
-            S.st[sFinal] = nfin;
-            S.st[sHave] = 0;
-            S.st[sLQ] = ~0u;
-            if (nk == kStEnd) S.st[sDone] = 1;
-            else S.st[sF] = np;
+            S.st[sNLong] = 0;  // (every thread read it before the kill barrier above)
         }
-        block_sync();
+        // (the next fill's barrier publishes T before the next candidates)
+        U[sOp] = op0 + total;
+        U[sEK] = nk;
+        U[sEP] = np;
+        U[sEJ] = nj;
+        U[sEA] = na;
+        U[sFinal] = nfin;
+        U[sHave] = 0;
+        U[sLQ] = ~0u;
+        if (nk == kStEnd) U[sDone] = 1;
+        else U[sF] = np;
     }
 
     // ---- 4. hits and match lengths of the positions whose candidate changed ----
@@ -879,7 +877,7 @@ struct Band {
             }
         }
         // the entry state's first event (uniform)
-        const uint32_t ek = S.st[sEK];
+        const uint32_t ek = U[sEK];
         block_sync();
         uint32_t e0;
         uint32_t jE = ~0u, jX = ~0u, qE = 0;  // entry search: first event / exit probe index
@@ -887,7 +885,7 @@ struct Band {
         if (ek == kStRem) {
             e0 = code(kNode, 0);
         } else {
-            const uint32_t j0 = S.st[sEJ];
+            const uint32_t j0 = U[sEJ];
             uint32_t ev = ~0u, exi = ~0u;
             for (uint32_t r = 0; r < kBS; ++r) {
                 const uint32_t j = j0 + t + kBT * r, x = probe_pos(j);
@@ -983,7 +981,7 @@ struct Band {
                 TK = kStEnd;
                 if (tv == kEntry) {
                     TF = jE == 0 ? f : probe_pos(jE) - probe_step(jE - 1);
-                    TA = S.st[sEA];
+                    TA = U[sEA];
                 } else {
                     const uint32_t s0 = f + tv + 1, qm = qmax_of(s0);
                     TF = qm >= s0 ? qm : s0;
@@ -994,7 +992,7 @@ struct Band {
                 if (tv == kEntry) {
                     TP = probe_pos(jX);
                     TJ = jX;
-                    TA = S.st[sEA];
+                    TA = U[sEA];
                 } else {
                     TP = f + kB;
                     TJ = f + kB - (f + tv + 1);
@@ -1038,7 +1036,7 @@ struct Band {
         uint32_t jlo = 0, jhi = 0;  // entry search probes [jlo, jhi] looked up
         bool ehit = false;
         if (ek == kStSrch) {
-            jlo = S.st[sEJ];
+            jlo = U[sEJ];
             const uint32_t jl = jE < jX ? jE : jX;
             jhi = jl;  // exclusive unless the event is a hit
             ehit = jE < jX && !eEnd;
@@ -1091,18 +1089,16 @@ struct Band {
                 S.ph[slot(x)] |= 0x80000000u;
             }
         }
-        block_sync();
-        if (t == 0) {
-            S.st[sTK] = TK;
-            S.st[sTP] = TP;
-            S.st[sTJ] = TJ;
-            S.st[sTA] = TA;
-            S.st[sTF] = TF;
-            S.st[sLQ] = LQ;
-            S.st[sLF] = LF;
-            S.st[sHave] = 1;
-        }
-        block_sync();
+        U[sTK] = TK;
+        U[sTP] = TP;
+        U[sTJ] = TJ;
+        U[sTA] = TA;
+        U[sTF] = TF;
+        U[sLQ] = LQ;
+        U[sLF] = LF;
+        U[sHave] = 1;
+        // (the entry probes' flags and every G bit reach the next pass's
+        // readers through its fill barrier)
     }
 };
 
@@ -1129,16 +1125,17 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
     Band<TT> B{S, im, n, n >= kMinLength ? n - kMfLimit : 0u, n >= kMinLength ? n - kLastLiterals : 0u, cap,
                cap < (uint32_t)(n + n / 255 + 16), out, pd, t, t >> 6, t & 63};
     for (uint32_t i = t; i < 4096; i += kBT) S.T[i] = 0;  // :548 (an empty slot reads as position 0)
-    if (t == 0) {
-        for (uint32_t i = 0; i < kStN; ++i) S.st[i] = 0;
-        S.st[sF] = 1;
-        S.st[sEK] = kStSrch;  // :280-282: put(0) (== the empty slot), search from 1
-        S.st[sEP] = 1;
-        S.st[sEJ] = 0;
-        S.st[sEA] = 0;
-        S.st[sFill] = 1;
-        S.st[sBFill] = 0;
-        S.st[sLQ] = ~0u;
+    if (t == 0) S.st[sNLong] = 0;
+    {
+        for (uint32_t i = 0; i < kStN; ++i) B.U[i] = 0;
+        B.U[sF] = 1;
+        B.U[sEK] = kStSrch;  // :280-282: put(0) (== the empty slot), search from 1
+        B.U[sEP] = 1;
+        B.U[sEJ] = 0;
+        B.U[sEA] = 0;
+        B.U[sFill] = 1;
+        B.U[sBFill] = 0;
+        B.U[sLQ] = ~0u;
     }
     block_sync();
     if (n >= kMinLength) {
@@ -1148,14 +1145,13 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
         uint32_t from = 0;  // positions whose candidate is to be resolved: >= from
         for (uint32_t pass = 0;; ++pass) {
             if (pass > 2 * n + 64) {
-                if (t == 0) S.st[sFail] = 1;
-                block_sync();
+                B.U[sFail] = 1;
                 break;
             }
             B.fill();
             if (kSt) st.lap(0);
             uint32_t cdl[kBS];
-            const bool have = S.st[sHave] != 0;
+            const bool have = B.U[sHave] != 0;
             B.cands(cdl, have ? 0u : from);
             if (kSt) st.lap(1);
             if (have) {
@@ -1166,7 +1162,7 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
                     st.lap(3);
                     st.acc[7]++;
                 }
-                if (S.st[sDone]) break;
+                if (B.U[sDone]) break;
                 from = f0 + kB;  // the positions new to the band
                 continue;
             }
@@ -1180,12 +1176,12 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
         }
     }
     // last literals (:500-530)
-    if (S.st[sFail]) {
+    if (B.U[sFail]) {
         if (t == 0) ret[0] = 0;
         return;
     }
-    const uint32_t anchor = n >= kMinLength ? S.st[sEA] : 0u;
-    const uint32_t R = n - anchor, op = S.st[sOp];
+    const uint32_t anchor = n >= kMinLength ? B.U[sEA] : 0u;
+    const uint32_t R = n - anchor, op = B.U[sOp];
     if (B.limited && (uint64_t)op + R + 1 + (R + 240) / 255 > cap) {
         if (t == 0) ret[0] = 0;
         return;
@@ -1209,7 +1205,7 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
     if (t == 0) {
         ret[0] = (int32_t)(lo + R);
         if (aux) {
-            aux[0] = n >= kMinLength ? S.st[sFinal] : 0u;
+            aux[0] = n >= kMinLength ? B.U[sFinal] : 0u;
             aux[1] = R;
         }
     }

@@ -93,6 +93,7 @@ static Blk B_;
 
 /* candidate of p under guess G (band [f, f+BW), G indexed p - f) */
 long g_hops[10];
+long g_mk[4], g_md[8];
 static uint32_t cand_of(const Blk *b, uint32_t f, const uint8_t *G, uint32_t p)
 {
 	uint32_t c = p, hops = 0;
@@ -108,6 +109,18 @@ static uint32_t cand_of(const Blk *b, uint32_t f, const uint8_t *G, uint32_t p)
 	return b->T[hashat(b, p)];
 }
 
+static int GUESS = 0;
+/* the first guess of a position new to the band */
+static uint8_t guess_new(const Blk *b, uint32_t p)
+{
+	if (GUESS == 0 || p < 2 || p > b->mflimit) return 1;
+	/* continuation of a full-population match at p-1 and p: an interior */
+	uint32_t d0 = b->pd[p], d1 = b->pd[p - 1];
+	int c0 = d0 && d0 == d1 && rd32(b, p - d0) == rd32(b, p);
+	int c1 = d1 && p - 1 >= d1 && rd32(b, p - 1 - d1) == rd32(b, p - 1);
+	if (GUESS == 1) return !(c0 && c1);
+	return !c0;
+}
 static int hit_of(const Blk *b, uint32_t p, uint32_t c, int rem)
 {
 	if ((rem || b->tt != LZ4E_TABLE_BYU16) && c + 65535 < p) return 0;
@@ -248,7 +261,7 @@ static int band_compress(Blk *b, uint8_t *out, Stats *st)
 		Chain ch = {malloc(sizeof(Look) * (BW + 8)), 0, malloc(sizeof(Seq) * (BW + 8)), 0,
 			    malloc(4 * (BW + 8)), s, malloc(BW)};
 		int have = 0;
-		memset(G, 1, BW);
+		for (uint32_t p = f; p < f + BW; p++) G[p - f] = guess_new(b, p);
 		for (;;) {
 			st->passes++;
 			/* 1. candidates under G */
@@ -260,7 +273,19 @@ static int band_compress(Blk *b, uint8_t *out, Stats *st)
 					const Look *L = &ch.lk[i];
 					uint32_t c = cand[L->pos - f];
 					int h = hit_of(b, L->pos, c, L->rem);
-					if (h != L->hit || (h && c != L->cand)) { bad = i; break; }
+					if (h != L->hit || (h && c != L->cand)) {
+						bad = i;
+						{
+							extern long g_mk[4], g_md[8];
+							uint32_t hiC = c > L->cand ? c : L->cand;
+							g_mk[c > L->cand ? 0 : 1]++;
+							uint32_t dd = L->pos - hiC;
+							g_md[dd < 16 ? 0 : dd < 64 ? 1 : dd < 256 ? 2 : dd < 1024 ? 3 : 4]++;
+							g_md[5] += L->pos - f;
+							g_md[6]++;
+						}
+						break;
+					}
 				}
 				St ns = bad < ch.nlk ? ch.lk[bad].before : ch.term;
 				if (bad < ch.nlk) st->mism++;
@@ -278,7 +303,7 @@ static int band_compress(Blk *b, uint8_t *out, Stats *st)
 				st->commits++;
 				if (ns.kind == K_END) break;
 				/* shift the band to [nf, nf + BW): keep G on the overlap */
-				memset(Gn, 1, BW);
+				for (uint32_t p = nf; p < nf + BW; p++) Gn[p - nf] = guess_new(b, p);
 				for (uint32_t p = nf; p < f + BW; p++) Gn[p - nf] = G[p - f];
 				memcpy(G, Gn, BW);
 				if (nf != f) {
@@ -328,6 +353,7 @@ int main(int argc, char **argv)
 	if (argc > 5) BW = (uint32_t)atoi(argv[5]);
 	if (argc > 6) FCAP = (uint32_t)atoi(argv[6]);
 	if (argc > 7) BCAP = (uint32_t)atoi(argv[7]);
+	if (argc > 8) GUESS = atoi(argv[8]);
 	Blk *b = &B_;
 	b->tt = tt; b->hlog = tt == LZ4E_TABLE_BYU64 ? 11 : tt == LZ4E_TABLE_BYU32 ? 12 : 13;
 	b->pd = malloc(2 * (size_t)bs + 64);
@@ -350,6 +376,8 @@ int main(int argc, char **argv)
 	       "slow/blk=%.1f lookups/pass=%.1f mism/blk=%.1f\n",
 	       argv[1], bs, tt, BW, FCAP, BCAP, nb, bad, (double)st.passes / nb, maxp, (double)st.longs / nb,
 	       (double)st.slows / nb, (double)st.lookups / st.passes, (double)st.mism / nb);
+	printf("mismatch: new cand later (put appeared) %ld, earlier (put vanished) %ld; lookup - changed cand: <16 %ld <64 %ld <256 %ld <1024 %ld more %ld; mean offset in band %.0f\n",
+	       g_mk[0], g_mk[1], g_md[0], g_md[1], g_md[2], g_md[3], g_md[4], (double)g_md[5] / (g_md[6] ? g_md[6] : 1));
 	printf("hops:"); for (int i = 1; i < 10; i++) printf(" %ld", g_hops[i]); printf("\n");
 	return bad != 0;
 }
