@@ -129,12 +129,13 @@ struct BandLds {
     uint16_t cd[kB];   // candidate delta hi[] was computed for (0: none)
     uint16_t nx[kB];   // scratch: ancestor links, segment exit codes
     uint16_t cn[kB];   // candidate delta under the current G (stable across a commit)
+    uint16_t an[kB];   // the last chain's latest node at or before a position (band offset + 1; 0: none)
     uint8_t gf[kB];    // flags of the last chain (kF*)
     uint64_t hmask[kSegs];        // hit positions per segment
     uint32_t segv[kSegs];         // block scan scratch
     uint32_t hfirst[kSegs + 1];   // first hit offset at or after each segment start
     uint16_t entry[kSegs];        // chain entry lane per segment (kNone: none)
-    uint32_t red[4];
+    uint32_t red[8];
     uint32_t st[kStN];
     uint32_t lng[3 * kLongLits];  // long literal runs: source, length, output position
     uint8_t by[kRing + kRingPad] __attribute__((aligned(16)));  // block byte p at p & (kRing - 1)
@@ -349,6 +350,18 @@ struct Band {
         const uint32_t r = S.red[0] | S.red[1] | S.red[2] | S.red[3];
         block_sync();
         return r;
+    }
+    // block minimum of two values at once (results in a, b)
+    LZ4E_DEV void block_min2(uint32_t& a, uint32_t& b) {
+        const uint32_t ma = lane_val(wave_scan(a, OpMin(), ~0u), 63), mb = lane_val(wave_scan(b, OpMin(), ~0u), 63);
+        if (lane == 0) {
+            S.red[w] = ma;
+            S.red[4 + w] = mb;
+        }
+        block_sync();
+        a = OpMin()(OpMin()(S.red[0], S.red[1]), OpMin()(S.red[2], S.red[3]));
+        b = OpMin()(OpMin()(S.red[4], S.red[5]), OpMin()(S.red[6], S.red[7]));
+        block_sync();
     }
     // Inclusive scan over the band in position order (slot s of thread t is
     // band offset 256 s + t: segment 4 s + wave, lane = place in it);
@@ -600,14 +613,11 @@ struct Band {
     LZ4E_DEV void commit(uint32_t bad, const uint32_t (&cdl)[kBS]) {
         const uint32_t f = F();
         const uint32_t ea = U[sEA];
-        // latest node at or before each position (offset + 1; 0: none)
+        // latest node at or before each position (offset + 1; 0: none), as
+        // the chain that made these lookups recorded it
         uint32_t an[kBS];
 #pragma unroll
-        for (uint32_t s = 0; s < kBS; ++s) {
-            const uint32_t o = 256 * s + t;
-            an[s] = (S.gf[rg(o)] & kFNode) ? o + 1 : 0u;
-        }
-        band_scan(an, OpMax(), 0u);
+        for (uint32_t s = 0; s < kBS; ++s) an[s] = S.an[rg(256 * s + t)];
         // sequences of the verified finding lookups
         Seq sq[kBS];
         uint32_t sz[kBS], ex[kBS];
@@ -616,7 +626,6 @@ struct Band {
             const uint32_t o = 256 * s + t;
             const uint32_t g = S.gf[rg(o)];
             sz[s] = 0;
-            if (bad != ~0u && o == bad) S.st[sBadA] = (g & kFNode) ? 0u : an[s];
             if (o < bad && (g & kFLook) && (g & kFHit)) {
                 // a probe is never a node, so its latest node is before it
                 const uint32_t a = an[s] ? f + an[s] - 1 : ea;
@@ -625,7 +634,7 @@ struct Band {
             }
             ex[s] = sz[s];
         }
-        const uint32_t total = band_scan(ex, OpAdd(), 0u);  // (its barriers publish sBadA)
+        const uint32_t total = band_scan(ex, OpAdd(), 0u);
         const uint32_t op0 = U[sOp];
         bool bad_fit = false;
         if (limited) {
@@ -686,7 +695,7 @@ struct Band {
                 na = x;
             } else {
                 nk = kStSrch;
-                const uint32_t ba = S.st[sBadA];
+                const uint32_t ba = (g & kFNode) ? 0u : S.an[rg(bad)];
                 if (ba) {
                     na = f + ba - 1;
                     nj = x - (na + 1);
@@ -868,17 +877,19 @@ struct Band {
             if (lane == 0) S.hmask[4 * s + w] = m;
         }
         block_sync();
-        if (t == 0) {
+        // first hit at or after each segment start: every wave writes the
+        // whole (identical) table itself, so it reads only its own writes
+        {
             uint32_t nxt = kNone;
-            S.hfirst[kSegs] = kNone;
             for (int k = kSegs - 1; k >= 0; --k) {
-                if (S.hmask[k]) nxt = 64 * (uint32_t)k + ctz64(S.hmask[k]);
-                S.hfirst[k] = nxt;
+                const uint64_t m = S.hmask[k];
+                if (m && (uint32_t)k >= lane) nxt = 64 * (uint32_t)k + ctz64(m);
             }
+            if (lane <= kSegs) S.hfirst[lane] = lane < kSegs ? nxt : kNone;
+            lockstep();
         }
         // the entry state's first event (uniform)
         const uint32_t ek = U[sEK];
-        block_sync();
         uint32_t e0;
         uint32_t jE = ~0u, jX = ~0u, qE = 0;  // entry search: first event / exit probe index
         bool eEnd = false;
@@ -895,8 +906,9 @@ struct Band {
                 }
                 if (x + probe_step(j) > mflimit || (S.hi[rg(x - f)] & 1)) ev = ev < j ? ev : j;
             }
-            jE = block_reduce(ev, OpMin(), ~0u);
-            jX = block_reduce(exi, OpMin(), ~0u);
+            block_min2(ev, exi);
+            jE = ev;
+            jX = exi;
             if (jE < jX) {
                 const uint32_t x = probe_pos(jE);
                 if (x + probe_step(jE) > mflimit) {
@@ -941,15 +953,24 @@ struct Band {
             S.nx[o] = (uint16_t)X;
         }
         block_sync();
-        if (t == 0) {
-            for (uint32_t k = 0; k < kSegs; ++k) S.entry[k] = (uint16_t)kNone;
-            uint32_t cur = e0;
-            while (ckind(cur) == kNode) {
-                const uint32_t o = cval(cur);
-                S.entry[o >> 6] = (uint16_t)(o & 63);
-                cur = S.nx[o];
+        // the stitch (wave 0): segment k's entry lane is where the chain
+        // enters it, the next entry is that lane's exit code; segments are
+        // entered in increasing order, so one unrolled pass over k
+        if (w == 0) {
+            uint32_t X[kSegs];
+#pragma unroll
+            for (uint32_t k = 0; k < kSegs; ++k) X[k] = S.nx[64 * k + lane];
+            uint32_t cur = e0, ent = kNone;
+#pragma unroll
+            for (uint32_t k = 0; k < kSegs; ++k) {
+                if (ckind(cur) == kNode && (cval(cur) >> 6) == k) {
+                    const uint32_t l = cval(cur) & 63u;
+                    ent = lane == k ? l : ent;
+                    cur = lane_val(X[k], l);
+                }
             }
-            S.st[sTerm] = cur;
+            if (lane < kSegs) S.entry[lane] = (uint16_t)ent;
+            if (lane == 0) S.st[sTerm] = cur;
         }
         block_sync();
         const uint32_t term = S.st[sTerm];
@@ -1033,6 +1054,8 @@ struct Band {
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s) an[s] = node[s] ? 256 * s + t + 1 : 0u;
         band_scan(an, OpMax(), 0u);  // (barriers: gf node flags published)
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) S.an[rg(256 * s + t)] = (uint16_t)an[s];
         uint32_t jlo = 0, jhi = 0;  // entry search probes [jlo, jhi] looked up
         bool ehit = false;
         if (ek == kStSrch) {
