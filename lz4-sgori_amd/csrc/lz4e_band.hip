@@ -54,7 +54,7 @@ constexpr uint32_t kSegs = kB / 64;   // 64-position segments (one per wave slot
 constexpr uint32_t kFCap = 32;        // match bytes compared per position (more: "long")
 constexpr uint32_t kBCap = 16;        // catch-up bytes compared per position
 constexpr uint32_t kFLong = 0xFFFFu;  // fwd field of a long match
-constexpr uint32_t kHops = 4;         // direct chain hops before pointer jumping
+constexpr uint32_t kHops = 6;         // direct chain hops before pointer jumping
 constexpr uint32_t kNone = 0xFFFFu;
 constexpr uint32_t kEntry = 0xFFFu;   // code value: the entry search (no node)
 constexpr uint32_t kLongLits = 8;     // long literal runs copied by the workgroup per commit
@@ -252,30 +252,55 @@ template <int TT>
 LZ4E_DEV void prev_block(const Img& im, uint32_t n, uint16_t* __restrict__ pd, uint32_t* last) {
     const uint32_t lane = lane_id();
     const uint32_t hlog = TT == kByU64 ? 11u : (TT == kByU32 ? 12u : 13u);
-    for (uint32_t i = lane; i < (1u << hlog); i += 64) last[i] = 0;
+    // table of (latest position + 1): u16 for byU16 (positions <= 65535:
+    // 65536 wraps to "none" only for the block's last hashed position, which
+    // nothing follows), u32 otherwise -- 16 KiB either way
+    uint16_t* last16 = (uint16_t*)last;
+    for (uint32_t i = lane; i < 4096; i += 64) last[i] = 0;
     lockstep();
     const uint32_t mflimit = n - kMfLimit;
     const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-    for (uint32_t base = 0; base <= mflimit; base += 64) {
-        const uint32_t p = base + lane;
-        const bool on = p <= mflimit;
-        const uint32_t h = on ? hash_at<TT>(im, p) : (1u << hlog) + lane;  // off lanes: unique keys
-        uint64_t m = ~0ull;
-        for (uint32_t k = 0; k <= hlog + 6; ++k) {
-            const bool bit = (h >> k) & 1;
-            const uint64_t bb = ballot(bit);
-            m &= bit ? bb : ~bb;
+    constexpr uint32_t kG = 8;  // chunks whose bytes are loaded together
+    for (uint32_t g0 = 0; g0 <= mflimit; g0 += 64 * kG) {
+        uint32_t wa[kG], wb[kG];
+#pragma unroll
+        for (uint32_t c = 0; c < kG; ++c) {
+            const uint32_t p = g0 + 64 * c + lane;
+            wa[c] = im.rd32(p);
+            wb[c] = TT == kByU32 ? im.rd32(p + 4) : 0u;
         }
-        const uint64_t lower = m & below;
-        const uint32_t prev_in = on ? last[h] : 0u;  // latest earlier chunk's position + 1
-        lockstep();
-        const bool group_last = ((m >> lane) >> 1) == 0;
-        if (on && group_last) last[h] = p + 1;
-        lockstep();
-        uint32_t d = 0;
-        if (lower) d = lane - (63 - (uint32_t)__builtin_clzll(lower));
-        else if (prev_in && p - (prev_in - 1) <= kMaxDistance) d = p - (prev_in - 1);
-        if (on) pd[p] = (uint16_t)d;
+#pragma unroll
+        for (uint32_t c = 0; c < kG; ++c) {
+            const uint32_t p = g0 + 64 * c + lane;
+            if (g0 + 64 * c > mflimit) break;
+            const bool on = p <= mflimit;
+            const uint32_t h = TT == kByU32 ? hash5((uint64_t)wa[c] | ((uint64_t)wb[c] << 32), 12)
+                                            : hash4(wa[c], hlog);
+            uint64_t m = ballot(on);
+            for (uint32_t k = 0; k < hlog; ++k) {
+                const bool bit = (h >> k) & 1;
+                const uint64_t bb = ballot(bit);
+                m &= bit ? bb : ~bb;
+            }
+            const uint64_t lower = m & below;
+            // latest earlier chunk's position + 1 (read before this chunk's writes)
+            const uint32_t prev_in = on ? (TT == kByU16 ? (uint32_t)last16[h] : last[h]) : 0u;
+            lockstep();
+            const bool group_last = ((m >> lane) >> 1) == 0;
+            if (on && group_last) {
+                if (TT == kByU16) last16[h] = (uint16_t)(p + 1);
+                else last[h] = p + 1;
+            }
+            lockstep();
+            uint32_t d = 0;
+            if (lower) {
+                d = lane - (63 - (uint32_t)__builtin_clzll(lower));
+            } else if (prev_in) {
+                const uint32_t q = TT == kByU16 ? prev_in - 1 : prev_in - 1;
+                if (p - q <= kMaxDistance) d = p - q;
+            }
+            if (on) pd[p] = (uint16_t)d;
+        }
     }
 }
 
@@ -283,7 +308,7 @@ __global__ __launch_bounds__(64) void prev_kernel(const uint8_t* __restrict__ sr
                                                   const uint32_t* __restrict__ src_len,
                                                   const uint8_t* __restrict__ table_type, uint16_t* __restrict__ pdbuf,
                                                   uint32_t max_len) {
-    __shared__ uint32_t last[8192];
+    __shared__ uint32_t last[4096];
     const uint32_t b = blockIdx.x;
     const uint32_t n = src_len[b];
     if (n < kMinLength || n > max_len) return;
@@ -441,37 +466,56 @@ struct Band {
     // together; only the positions new to the band are resolved then.
     LZ4E_DEV void cands(uint32_t (&cdl)[kBS], uint32_t from) {
         const uint32_t f = F();
-        uint32_t pend = 0, mine = 0;
+        uint32_t pend = 0, mine = 0, tab = 0;
+        uint32_t c[kBS], d[kBS], e[kBS];
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s) {
             const uint32_t o = 256 * s + t, p = f + o;
             cdl[s] = 0;
+            c[s] = o;
+            d[s] = 0;
+            e[s] = 0;
             if (p > mflimit) continue;
             if (p < from) {
                 cdl[s] = S.cn[slot(p)];
                 continue;
             }
             mine |= 1u << s;
-            const uint32_t e = S.ph[slot(p)];
-            uint32_t c = o, d = e & 0xFFFFu;
-            uint32_t how = 2;  // 0 resolved in band, 1 table, 2 pending
-            for (uint32_t k = 0; k < kHops; ++k) {
-                if (d == 0 || d > c) {
-                    how = 1;
-                    break;
-                }
-                c -= d;
-                const uint32_t ec = S.ph[slot(f + c)];
-                if (ec >> 31) {
-                    how = 0;
-                    break;
-                }
-                d = ec & 0xFFFFu;
-            }
-            if (how == 0) cdl[s] = o - c;
-            else if (how == 1) cdl[s] = from_table(p, e);
-            else pend |= 1u << s;
+            e[s] = S.ph[slot(p)];
+            d[s] = e[s] & 0xFFFFu;
         }
+        // the chain walks, hop by hop for all four slots at once
+        uint32_t walk = mine;
+#pragma unroll
+        for (uint32_t k = 0; k < kHops; ++k) {
+            uint32_t ec[kBS];
+#pragma unroll
+            for (uint32_t s = 0; s < kBS; ++s) {
+                ec[s] = 0;
+                if (!((walk >> s) & 1)) continue;
+                if (d[s] == 0 || d[s] > c[s]) {
+                    walk &= ~(1u << s);
+                    tab |= 1u << s;
+                    continue;
+                }
+                c[s] -= d[s];
+                ec[s] = S.ph[slot(f + c[s])];
+            }
+#pragma unroll
+            for (uint32_t s = 0; s < kBS; ++s) {
+                if (!((walk >> s) & 1)) continue;
+                if (ec[s] >> 31) {
+                    walk &= ~(1u << s);
+                    cdl[s] = 256 * s + t - c[s];
+                } else {
+                    d[s] = ec[s] & 0xFFFFu;
+                }
+            }
+        }
+        pend = walk;
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s)
+            if ((tab >> s) & 1) cdl[s] = from_table(f + 256 * s + t, e[s]);
         if (block_any(pend != 0)) resolve_pending(cdl, pend);
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s)
@@ -480,7 +524,8 @@ struct Band {
     LZ4E_DEV void resolve_pending(uint32_t (&cdl)[kBS], uint32_t pend) {
         const uint32_t f = F();
         // pointer jumping over every band position: nx[o] = an ancestor with
-        // only unmarked chain positions between (kNone: none in the band)
+        // only unmarked chain positions between (kNone: none in the band);
+        // one barrier per round (the flags alternate halves of red[])
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s) {
             const uint32_t o = 256 * s + t, p = f + o;
@@ -488,19 +533,26 @@ struct Band {
             S.nx[o] = (uint16_t)((d == 0 || d > o) ? kNone : o - d);
         }
         block_sync();
-        for (;;) {
+        for (uint32_t r = 0;; ++r) {
+            uint32_t a[kBS], m[kBS], a2[kBS];
+#pragma unroll
+            for (uint32_t s = 0; s < kBS; ++s) a[s] = S.nx[256 * s + t];
+#pragma unroll
+            for (uint32_t s = 0; s < kBS; ++s) m[s] = a[s] == kNone ? 0x80000000u : S.ph[slot(f + a[s])];
+#pragma unroll
+            for (uint32_t s = 0; s < kBS; ++s) a2[s] = (m[s] >> 31) ? a[s] : S.nx[a[s]];
             bool more = false;
 #pragma unroll
             for (uint32_t s = 0; s < kBS; ++s) {
-                const uint32_t o = 256 * s + t;
-                const uint32_t a = S.nx[o];
-                if (a == kNone || (S.ph[slot(f + a)] >> 31)) continue;
-                const uint32_t a2 = S.nx[a];
-                S.nx[o] = (uint16_t)a2;
-                more |= a2 != kNone;
+                if (a2[s] == a[s]) continue;
+                S.nx[256 * s + t] = (uint16_t)a2[s];
+                more |= a2[s] != kNone;
             }
+            const uint32_t h = 4 * (r & 1);
+            const uint32_t any = ballot(more) != 0;
+            if (lane == 0) S.red[h + w] = any;
             block_sync();
-            if (!block_any(more)) break;
+            if (!(S.red[h] | S.red[h + 1] | S.red[h + 2] | S.red[h + 3])) break;
         }
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s) {
@@ -847,6 +899,56 @@ struct Band {
         return end < kB ? code(kNode, end) : code(kExitRem, o);
     }
 
+    // next codes of my four slots, each phase's LDS reads issued for all
+    // slots before any is used (the same result as next_code per slot)
+    LZ4E_DEV void next_codes(uint32_t (&cc)[kBS]) const {
+        const uint32_t f = F();
+        uint32_t h[kBS], q[kBS], hq[kBS];
+        uint64_t m[kBS];
+        uint32_t nf[kBS];
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) h[s] = S.hi[rg(256 * s + t)];
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t y = 256 * s + t + 1, k = y >> 6;
+            m[s] = y < kB ? S.hmask[k] >> (y & 63) : 0ull;
+            nf[s] = y < kB ? S.hfirst[k + 1] : kNone;
+        }
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t, y = o + 1;
+            q[s] = (h[s] & 1) ? o : (m[s] ? y + ctz64(m[s]) : nf[s]);
+            hq[s] = q[s] < kB ? S.hi[rg(q[s])] : 0u;
+        }
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t, e = f + o;
+            uint32_t c;
+            if (e > mflimit) {
+                c = code(kEndRem, o);
+            } else {
+                bool srch_end = false;
+                if (!(h[s] & 1)) {
+                    const uint32_t s0 = e + 1, qm = qmax_of(s0);
+                    if (q[s] == kNone || f + q[s] > qm) {
+                        srch_end = true;
+                        c = (qm < f + kB || qm < s0) ? ((s0 + 65 + 2 <= mflimit) ? code(kSlow, o) : code(kEndLim, o))
+                                                     : code(kExitSrch, o);
+                    }
+                }
+                if (!srch_end) {
+                    const uint32_t fw = hq[s] >> 16;
+                    if (fw == kFLong) c = code(kLong, o);
+                    else {
+                        const uint32_t end = q[s] + 4 + fw;
+                        c = end < kB ? code(kNode, end) : code(kExitRem, o);
+                    }
+                }
+            }
+            cc[s] = c;
+        }
+    }
+
     // Exact match length from q + 4 against q - d + 4 (the whole workgroup).
     LZ4E_DEV uint32_t fwd_exact(uint32_t q, uint32_t d) {
         const uint32_t c = q - d, lim = q + 4 < matchlimit ? matchlimit - (q + 4) : 0u;
@@ -929,29 +1031,33 @@ struct Band {
         }
         // in-segment pointer doubling: J (next lane, 64: left the segment),
         // M (lanes visited), X (the exit code)
-        uint32_t Mlo[kBS], Mhi[kBS];
+        uint32_t Mlo[kBS], Mhi[kBS], J[kBS], X[kBS];
+        next_codes(X);
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s) {
-            const uint32_t o = 256 * s + t;
-            const uint32_t c = next_code(o);
-            uint32_t J = (ckind(c) == kNode && (cval(c) >> 6) == (o >> 6)) ? cval(c) & 63u : 64u;
-            uint32_t X = c;
+            const uint32_t o = 256 * s + t, c = X[s];
+            J[s] = (ckind(c) == kNode && (cval(c) >> 6) == (o >> 6)) ? cval(c) & 63u : 64u;
             Mlo[s] = lane < 32 ? 1u << lane : 0u;
             Mhi[s] = lane >= 32 ? 1u << (lane - 32) : 0u;
+        }
+        // (rounds outer, slots inner: four independent permute chains)
 #pragma unroll
-            for (uint32_t r = 0; r < 6; ++r) {
-                const uint32_t src = J < 64 ? J : lane;
-                const uint32_t Jn = shfl(J, src), Xn = shfl(X, src);
+        for (uint32_t r = 0; r < 6; ++r) {
+#pragma unroll
+            for (uint32_t s = 0; s < kBS; ++s) {
+                const uint32_t src = J[s] < 64 ? J[s] : lane;
+                const uint32_t Jn = shfl(J[s], src), Xn = shfl(X[s], src);
                 const uint32_t Ln = shfl(Mlo[s], src), Hn = shfl(Mhi[s], src);
-                if (J < 64) {
-                    J = Jn;
-                    X = Xn;
+                if (J[s] < 64) {
+                    J[s] = Jn;
+                    X[s] = Xn;
                     Mlo[s] |= Ln;
                     Mhi[s] |= Hn;
                 }
             }
-            S.nx[o] = (uint16_t)X;
         }
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) S.nx[256 * s + t] = (uint16_t)X[s];
         block_sync();
         // the stitch (wave 0): segment k's entry lane is where the chain
         // enters it, the next entry is that lane's exit code; segments are
@@ -1065,38 +1171,46 @@ struct Band {
             ehit = jE < jX && !eEnd;
             if (ehit) jhi = jE + 1;
         }
+        // (every slot's LDS reads first, then the flags)
+        uint32_t h[kBS], hv[kBS], g2[kBS], eph[kBS], nfv[kBS];
+        uint64_t mv[kBS];
+#pragma unroll
+        for (uint32_t s = 0; s < kBS; ++s) {
+            const uint32_t o = 256 * s + t, p = f + o;
+            const uint32_t v = an[s] ? an[s] - 1 : 0u, y = v + 1, k = y >> 6;
+            h[s] = S.hi[rg(o)];
+            hv[s] = S.hi[rg(v)];
+            g2[s] = o + 2 < kB ? S.gf[rg(o + 2)] : 0u;
+            eph[s] = S.ph[slot(p)];
+            mv[s] = y < kB ? S.hmask[k] >> (y & 63) : 0ull;
+            nfv[s] = y < kB ? S.hfirst[k + 1] : kNone;
+        }
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s) {
             const uint32_t o = 256 * s + t, p = f + o;
             uint32_t g = 0;
             bool put = false;
             if (o < tpo && p <= mflimit) {
-                const uint32_t h = S.hi[rg(o)];
                 if (node[s]) {
-                    g = kFNode | kFLook | kFRem | ((h & 1) ? kFHit : 0u);
+                    g = kFNode | kFLook | kFRem | ((h[s] & 1) ? kFHit : 0u);
                     put = true;
                 } else if (an[s]) {
                     const uint32_t v = an[s] - 1;  // the latest node, before o
-                    if (f + v <= mflimit && !(S.hi[rg(v)] & 1)) {
+                    if (f + v <= mflimit && !(hv[s] & 1)) {
                         const uint32_t s0 = f + v + 1, qm = qmax_of(s0);
-                        const uint32_t y = nh(v + 1);
+                        const uint32_t y = mv[s] ? v + 1 + ctz64(mv[s]) : nfv[s];
                         const uint32_t lim = (y != kNone && f + y <= qm) ? f + y : qm;
                         if (p <= lim && qm >= s0) {
-                            g = kFLook | ((h & 1) ? kFHit : 0u);
+                            g = kFLook | ((h[s] & 1) ? kFHit : 0u);
                             put = true;
                         }
                     }
                 }
-                if (o + 2 < kB && (S.gf[rg(o + 2)] & kFNode) && p + 2 <= mflimit) put = true;
+                if ((g2[s] & kFNode) && p + 2 <= mflimit) put = true;
                 if (TK == kStRem && p + 2 == TP) put = true;
-            } else if (node[s]) {
-                g = kFNode;  // a node past mflimit (the end) or at the end state
             }
-            g |= (uint32_t)(S.gf[rg(o)] & kFNode);
-            if (o < tpo) {
-                const uint32_t e = S.ph[slot(p)];
-                S.ph[slot(p)] = (e & 0x7FFFFFFFu) | (put ? 0x80000000u : 0u);
-            }
+            if (node[s]) g |= kFNode;  // (also a node past mflimit or at the end state)
+            if (o < tpo) S.ph[slot(p)] = (eph[s] & 0x7FFFFFFFu) | (put ? 0x80000000u : 0u);
             S.gf[rg(o)] = (uint8_t)g;
         }
         block_sync();

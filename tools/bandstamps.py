@@ -74,6 +74,22 @@ def main():
     per = d[:, :6].sum(0) / max(d[:, 6].sum(), 1)
     print("  cycles per chain pass: " + ", ".join(f"{PH[i]} {per[i]:.0f}" for i in range(6)) +
           f"  (total {per.sum():.0f})")
+    if wl == "silesia":
+        names = ["text", "ints", "runs", "random", "jpeg", "records"]
+        cls_of = np.random.default_rng(0x5157).choice(6, size=3234, p=[0.40, 0.15, 0.10, 0.10, 0.10, 0.15])[:n]
+        for c in range(6):
+            m = cls_of == c
+            if m.any():
+                pc = d[m, :6].sum(0) / max(d[m, 6].sum(), 1)
+                print(f"  {names[c]:8s} n={m.sum():4d} cycles/block {tot[m].mean():10.0f} max {tot[m].max():10.0f} "
+                      f"passes {d[m, 6].mean():6.1f}; per pass " + ", ".join(f"{PH[i]} {pc[i]:.0f}" for i in range(6)))
+        texts = np.nonzero(cls_of == 0)[0]
+        if texts.size:
+            i = int(texts[0])
+            msi, di = stamped(slice(i, i + 1), 1)
+            pp = di[0, :6] / max(di[0, 6], 1)
+            print(f"  text block {i} alone: {msi:.3f} ms, {di[0, :6].sum():.0f} cycles, passes {di[0, 6]:.0f}; per pass "
+                  + ", ".join(f"{PH[k]} {pp[k]:.0f}" for k in range(6)))
     order = np.argsort(d[:, 6])[::-1][:4]
     for i in order:
         i = int(i)
