@@ -1319,17 +1319,6 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
     return e ? (uint32_t)strtoul(e, nullptr, 10) : dflt;
 }
 
-// Compressor for batches of blocks larger than kMaxLdsInput without a
-// dictionary: 'b' the band compressor (lz4e_band.hip, default), 'w' the
-// one-wave-per-block compressor; LZ4E_COMPRESS_MODE=band|wave overrides.
-char compress_mode() {
-    static const char m = [] {
-        const char* e = getenv("LZ4E_COMPRESS_MODE");
-        return e && e[0] == 'w' ? 'w' : 'b';
-    }();
-    return m;
-}
-
 template <bool kStamps>
 hipError_t launch_compress_impl(const CompressBatch& a, hipStream_t stream, uint64_t* dbg) {
     if (a.nblocks == 0) return hipSuccess;
@@ -1360,16 +1349,11 @@ hipError_t launch_compress_impl(const CompressBatch& a, hipStream_t stream, uint
         (void)hipGetLastError();  // a failed pool allocation only costs the ordering
         scratch = nullptr;
     }
-    hipError_t err;
-    if (!kStamps && a.dict_len == nullptr && compress_mode() == 'b') {
-        err = launch_compress_band(a, stream, scratch ? (const uint32_t*)(scratch + a.nblocks) : nullptr);
-    } else {
-        hipLaunchKernelGGL((compress_kernel<false, kStamps>), grid, block, lds, stream, a.src,
-                           a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
-                           a.aux, a.nblocks, a.max_len, dbg, a.dict_len,
-                           scratch ? (const uint32_t*)(scratch + a.nblocks) : nullptr);
-        err = hipGetLastError();
-    }
+    hipLaunchKernelGGL((compress_kernel<false, kStamps>), grid, block, lds, stream, a.src,
+                       a.src_off, a.src_len, a.table_type, a.dst, a.dst_off, a.dst_cap, a.ret,
+                       a.aux, a.nblocks, a.max_len, dbg, a.dict_len,
+                       scratch ? (const uint32_t*)(scratch + a.nblocks) : nullptr);
+    const hipError_t err = hipGetLastError();
     if (scratch) (void)hipFreeAsync(scratch, stream);
     return err;
 }

@@ -60,11 +60,6 @@ enum : int { kOrderNever = 0, kOrderAuto = 1, kOrderAlways = 2 };
 int launch_order_mode(bool compress);
 
 uint32_t compress_lds_bytes(uint32_t max_len, bool lds_input);
-// The band-parallel compressor (lz4e_band.hip): one 256-thread workgroup
-// per block, blocks in `order` (nullable); not for dictionary batches.
-// dbg (nullable): the stamped build, 8 x u64 per block (lz4e_band.hip).
-hipError_t launch_compress_band(const CompressBatch& a, hipStream_t stream, const uint32_t* order,
-                                uint64_t* dbg = nullptr);
 hipError_t launch_compress(const CompressBatch& a, hipStream_t stream);
 // Diagnostic build: per-block phase cycle counters (8 x u64 per block) into dbg.
 hipError_t launch_compress_stamped(const CompressBatch& a, hipStream_t stream, uint64_t* dbg);

@@ -864,20 +864,6 @@ int lz4e_debug_compress_stamped(const uint8_t* src, const uint64_t* src_off, con
                : -1;
 }
 
-// Diagnostic (not part of include/lz4e.h): the band compressor's stamped
-// build (dbg: 8 x u64 per block, zeroed by the caller; tools/bandstamps.py).
-int lz4e_debug_compress_band(const uint8_t* src, const uint64_t* src_off, const uint32_t* src_len,
-                             const uint8_t* table_type, uint8_t* dst, const uint64_t* dst_off,
-                             const uint32_t* dst_cap, int32_t* ret, uint32_t nblocks, uint32_t max_len,
-                             void* stream, uint64_t* dbg) {
-    lz4e::CompressBatch a{src, src_off, src_len, table_type, dst, dst_off, dst_cap, ret, nullptr,
-                          nblocks, max_len};
-    return hip_ok(lz4e::launch_compress_band(a, static_cast<hipStream_t>(stream), nullptr, dbg),
-                  "band compress launch")
-               ? 0
-               : -1;
-}
-
 // Diagnostic (not part of include/lz4e.h): clock_probe_kernel on `stream`
 // (out: 3 x u64 in device memory: delta s_memtime, delta s_memrealtime, junk).
 int lz4e_debug_clock_probe(void* stream, uint64_t* out, uint32_t iters) {

@@ -50,7 +50,7 @@ def main():
     src = torch.from_numpy(np.ascontiguousarray(data[:n * bs])).to(dev)
     dst = torch.zeros(n * slot, dtype=torch.uint8, device=dev)
     ret = torch.zeros(n, dtype=torch.int32, device=dev)
-    dbg = torch.zeros(n * 8, dtype=torch.int64, device=dev)
+    dbg = torch.zeros(n * 16, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream().cuda_stream
 
     def stamped(sl=slice(None), k=n):
@@ -63,7 +63,7 @@ def main():
         e1.record()
         assert r == 0
         torch.cuda.synchronize()
-        return e0.elapsed_time(e1), dbg[:8 * k].cpu().numpy().reshape(k, 8).astype(np.float64)
+        return e0.elapsed_time(e1), dbg[:16 * k].cpu().numpy().reshape(k, 16).astype(np.float64)
 
     stamped()
     ms, d = stamped()
@@ -74,6 +74,9 @@ def main():
     per = d[:, :6].sum(0) / max(d[:, 6].sum(), 1)
     print("  cycles per chain pass: " + ", ".join(f"{PH[i]} {per[i]:.0f}" for i in range(6)) +
           f"  (total {per.sum():.0f})")
+    CH = ["masks", "entry", "next", "doubling", "stitch", "end", "nodescan", "flags"]
+    chs = d[:, 8:16].sum(0) / max(d[:, 6].sum(), 1)
+    print("  chain split per pass: " + ", ".join(f"{CH[i]} {chs[i]:.0f}" for i in range(8)))
     if wl == "silesia":
         names = ["text", "ints", "runs", "random", "jpeg", "records"]
         cls_of = np.random.default_rng(0x5157).choice(6, size=3234, p=[0.40, 0.15, 0.10, 0.10, 0.10, 0.15])[:n]
@@ -90,6 +93,8 @@ def main():
             pp = di[0, :6] / max(di[0, 6], 1)
             print(f"  text block {i} alone: {msi:.3f} ms, {di[0, :6].sum():.0f} cycles, passes {di[0, 6]:.0f}; per pass "
                   + ", ".join(f"{PH[k]} {pp[k]:.0f}" for k in range(6)))
+            cs = di[0, 8:16] / max(di[0, 6], 1)
+            print("    chain split: " + ", ".join(f"{CH[k]} {cs[k]:.0f}" for k in range(8)))
     order = np.argsort(d[:, 6])[::-1][:4]
     for i in order:
         i = int(i)

@@ -1,4 +1,17 @@
-// lz4e_band.hip -- gfx950 band-parallel LZ4E compressor (round 5).
+// lz4e_band.hip -- gfx950 band-parallel LZ4E compressor (round 5 EXPERIMENT,
+// not built into the library; DESIGN.md §3 "Band compressor (experiment)").
+//
+// Result: bit-exact on the GPU (every compress parity test and every frame
+// of the full-size configs against the oracle), but 5.6x SLOWER than the
+// one-wave compressor (silesia64k compress 19.6 vs 3.5 ms): per pass every
+// wave re-runs ~80 instructions per band position (candidate walks, hit
+// tests, next codes, in-segment pointer doubling, scans, flags) while a pass
+// commits ~480 of the 1024 positions, ~14x the one-wave kernel's
+// instructions per input byte, and the kernel is issue-bound
+// (profiles/r05/band_stamps.txt).  Kept as the record of the experiment:
+// tools/bandexp/bandmodel.c (CPU model, pass counts), build_band.sh +
+// test_emulator_band.py (sanitized lane emulator vs the oracle),
+// bandstamps.py (per-phase cycles).
 //
 // Restates LZ4E_compress_generic (/root/reference/lz4e/lz4e_compress.c:218-534,
 // noDict, acceleration 1) bit-exactly with one 256-thread workgroup per
@@ -322,6 +335,28 @@ __global__ __launch_bounds__(64) void prev_kernel(const uint8_t* __restrict__ sr
 
 // ---- the band kernel ----------------------------------------------------------
 
+// Stamped build (kSt): per block, thread 0's shader cycles per phase and the
+// pass counts (dbg[0..7]: fill, cands, verify, commit, hits, chain, passes,
+// commits), and the chain phase split (dbg[8..15]: hit masks, entry search,
+// next codes, doubling, stitch, end state, node scan, flags;
+// lz4e_debug_compress_band, tools/bandstamps.py).
+struct BandStamps {
+    uint64_t acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t t0 = 0, t1 = 0;
+    LZ4E_DEV void start() { t0 = t1 = clock64(); }
+    LZ4E_DEV void lap(uint32_t k) {
+        const uint64_t x = clock64();
+        acc[k] += x - t0;
+        t0 = x;
+    }
+    LZ4E_DEV void mark() { t1 = clock64(); }
+    LZ4E_DEV void sub(uint32_t k) {
+        const uint64_t x = clock64();
+        acc[8 + k] += x - t1;
+        t1 = x;
+    }
+};
+
 template <int TT>
 struct Band {
     BandLds& S;
@@ -334,6 +369,13 @@ struct Band {
     // uniform parse state: every thread keeps the same copy (values from
     // LDS read after a barrier, block reductions, or computed from them)
     uint32_t U[kStN];
+    BandStamps* sp = nullptr;  // the stamped build's counters (thread 0 reads them)
+    LZ4E_DEV void smark() {
+        if (sp) sp->mark();
+    }
+    LZ4E_DEV void ssub(uint32_t k) {
+        if (sp) sp->sub(k);
+    }
 
     LZ4E_DEV static uint32_t slot(uint32_t p) { return p & (kB - 1); }
     LZ4E_DEV uint32_t F() const { return U[sF]; }
@@ -968,6 +1010,7 @@ struct Band {
 
     // ---- 6-7. the chain from the entry state; flags and the next guess ----
     LZ4E_DEV void chain() {
+        smark();
         const uint32_t f = F();
         // hit masks per segment
         uint32_t hb[kBS];
@@ -979,6 +1022,7 @@ struct Band {
             if (lane == 0) S.hmask[4 * s + w] = m;
         }
         block_sync();
+        ssub(0);
         // first hit at or after each segment start: every wave writes the
         // whole (identical) table itself, so it reads only its own writes
         {
@@ -1029,10 +1073,12 @@ struct Band {
                 e0 = code(kExitSrch, kEntry);
             }
         }
+        ssub(1);
         // in-segment pointer doubling: J (next lane, 64: left the segment),
         // M (lanes visited), X (the exit code)
         uint32_t Mlo[kBS], Mhi[kBS], J[kBS], X[kBS];
         next_codes(X);
+        ssub(2);
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s) {
             const uint32_t o = 256 * s + t, c = X[s];
@@ -1059,6 +1105,7 @@ struct Band {
 #pragma unroll
         for (uint32_t s = 0; s < kBS; ++s) S.nx[256 * s + t] = (uint16_t)X[s];
         block_sync();
+        ssub(3);
         // the stitch (wave 0): segment k's entry lane is where the chain
         // enters it, the next entry is that lane's exit code; segments are
         // entered in increasing order, so one unrolled pass over k
@@ -1080,6 +1127,7 @@ struct Band {
         }
         block_sync();
         const uint32_t term = S.st[sTerm];
+        ssub(4);
         // node flags of my positions
         uint32_t node[kBS];
 #pragma unroll
@@ -1147,6 +1195,7 @@ struct Band {
                 }
             }
         }
+        ssub(5);
         // the end state's position: flags below it, G kept at and above it
         const uint32_t tpo = TK == kStEnd ? kB : (TP - f < kB ? TP - f : kB);
         // node flags to LDS (puts at e - 2 read the neighbours')
@@ -1171,6 +1220,7 @@ struct Band {
             ehit = jE < jX && !eEnd;
             if (ehit) jhi = jE + 1;
         }
+        ssub(6);
         // (every slot's LDS reads first, then the flags)
         uint32_t h[kBS], hv[kBS], g2[kBS], eph[kBS], nfv[kBS];
         uint64_t mv[kBS];
@@ -1226,6 +1276,7 @@ struct Band {
                 S.ph[slot(x)] |= 0x80000000u;
             }
         }
+        ssub(7);
         U[sTK] = TK;
         U[sTP] = TP;
         U[sTJ] = TJ;
@@ -1239,20 +1290,6 @@ struct Band {
     }
 };
 
-// Stamped build (kSt): per block, thread 0's shader cycles per phase and the
-// pass counts (dbg[0..7]: fill, cands, verify, commit, hits, chain, passes,
-// commits; lz4e_debug_compress_band, tools/bandstamps.py).
-struct BandStamps {
-    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t t0 = 0;
-    LZ4E_DEV void start() { t0 = clock64(); }
-    LZ4E_DEV void lap(uint32_t k) {
-        const uint64_t t1 = clock64();
-        acc[k] += t1 - t0;
-        t0 = t1;
-    }
-};
-
 template <int TT, bool kSt>
 LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, uint32_t cap, const uint16_t* pd,
                          int32_t* ret, uint32_t* aux, uint64_t* dbg) {
@@ -1263,6 +1300,7 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
                cap < (uint32_t)(n + n / 255 + 16), out, pd, t, t >> 6, t & 63};
     for (uint32_t i = t; i < 4096; i += kBT) S.T[i] = 0;  // :548 (an empty slot reads as position 0)
     if (t == 0) S.st[sNLong] = 0;
+    if (kSt) B.sp = &st;
     {
         for (uint32_t i = 0; i < kStN; ++i) B.U[i] = 0;
         B.U[sF] = 1;
@@ -1338,7 +1376,7 @@ LZ4E_DEV void band_block(BandLds& S, const Img& im, uint32_t n, uint8_t* out, ui
     }
     B.copy_lits_wg(lo, anchor, R);
     if (kSt && t == 0 && dbg)
-        for (uint32_t k = 0; k < 8; ++k) dbg[k] = st.acc[k];
+        for (uint32_t k = 0; k < 16; ++k) dbg[k] = st.acc[k];
     if (t == 0) {
         ret[0] = (int32_t)(lo + R);
         if (aux) {
@@ -1369,7 +1407,7 @@ __global__ __launch_bounds__(kBT, LZ4E_BAND_WAVES) void band_kernel(const uint8_
     const uint16_t* pd = pdbuf + (size_t)b * max_len;
     uint32_t* ax = aux ? aux + 2 * (size_t)b : nullptr;
     const int tt = table_type[b];
-    uint64_t* d = kSt && dbg ? dbg + 8 * (size_t)b : nullptr;
+    uint64_t* d = kSt && dbg ? dbg + 16 * (size_t)b : nullptr;
     if (tt == kByU32) band_block<kByU32, kSt>(S, im, n, out, dst_cap[b], pd, ret + b, ax, d);
     else if (tt == kByU64) band_block<kByU64, kSt>(S, im, n, out, dst_cap[b], pd, ret + b, ax, d);
     else band_block<kByU16, kSt>(S, im, n, out, dst_cap[b], pd, ret + b, ax, d);

@@ -1,4 +1,7 @@
-"""The band compressor's own source (csrc/lz4e_band.hip) on the CPU lane
+"""(Experiment record, not collected by the suite: run it explicitly with
+python -m pytest tools/bandexp/test_emulator_band.py.)
+
+The band compressor's own source (tools/bandexp/lz4e_band.hip) on the CPU lane
 emulator under ASan + UBSan: every frame, its size and the iterator
 post-state words equal the oracle's (tools/emu/emu_band_main.cpp), on the
 block kinds whose parses exercise each of its paths -- short chains (text),
@@ -14,7 +17,7 @@ import pytest
 
 from lz4e_amd import BYU16, BYU32, BYU64, corpus
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CXX = "/opt/rocm/llvm/bin/clang++"
 
 
@@ -24,7 +27,7 @@ def band_exe(tmp_path_factory):
         pytest.skip("no clang++ for the emulator")
     b = tmp_path_factory.mktemp("emuband")
     exe = str(b / "emu_band_main")
-    subprocess.run(["bash", os.path.join(REPO, "tools", "emu", "build_band.sh"), exe,
+    subprocess.run(["bash", os.path.join(REPO, "tools", "bandexp", "build_band.sh"), exe,
                     "-fsanitize=address,undefined", "-fno-sanitize=alignment", "-fno-sanitize-recover=all"],
                    check=True, capture_output=True)
     yield exe
