@@ -17,15 +17,16 @@ import sys
 import numpy as np
 import torch
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "lz4-sgori_amd"))
 import lz4e_amd  # noqa: E402
 from lz4e_amd import corpus  # noqa: E402
 
-L = lz4e_amd.lib()
+lz4e_amd.lib()  # (HIP runtime up)
+L = ctypes.CDLL(os.environ.get("BAND_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "libband.so")))
 P = ctypes.c_void_p
-L.lz4e_debug_compress_band.argtypes = [P] * 8 + [ctypes.c_uint32, ctypes.c_uint32, P, P]
-L.lz4e_debug_compress_band.restype = ctypes.c_int
+L.band_compress_dev.argtypes = [P] * 8 + [ctypes.c_uint32, ctypes.c_uint32, P, P]
+L.band_compress_dev.restype = ctypes.c_int
 PH = ["fill", "cands", "verify", "commit", "hits", "chain"]
 
 
@@ -57,7 +58,7 @@ def main():
         dbg.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        r = L.lz4e_debug_compress_band(src.data_ptr(), offs[sl].data_ptr(), lens[sl].data_ptr(), tt[sl].data_ptr(),
+        r = L.band_compress_dev(src.data_ptr(), offs[sl].data_ptr(), lens[sl].data_ptr(), tt[sl].data_ptr(),
                                        dst.data_ptr(), doffs[sl].data_ptr(), caps[sl].data_ptr(), ret[sl].data_ptr(),
                                        k, bs, s, dbg.data_ptr())
         e1.record()

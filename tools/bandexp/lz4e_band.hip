@@ -60,7 +60,10 @@ namespace lz4e {
 
 namespace {
 
-constexpr uint32_t kB = 1024;         // band width (positions)
+#ifndef LZ4E_BAND_B
+#define LZ4E_BAND_B 1024
+#endif
+constexpr uint32_t kB = LZ4E_BAND_B;  // band width (positions; 512 or 1024)
 constexpr uint32_t kBT = 256;         // threads per workgroup (4 waves)
 constexpr uint32_t kBS = kB / kBT;    // band slots per thread
 constexpr uint32_t kSegs = kB / 64;   // 64-position segments (one per wave slot)
@@ -1408,9 +1411,14 @@ __global__ __launch_bounds__(kBT, LZ4E_BAND_WAVES) void band_kernel(const uint8_
     uint32_t* ax = aux ? aux + 2 * (size_t)b : nullptr;
     const int tt = table_type[b];
     uint64_t* d = kSt && dbg ? dbg + 16 * (size_t)b : nullptr;
+#ifdef LZ4E_BAND_ONLY_U16
+    (void)tt;
+    band_block<kByU16, kSt>(S, im, n, out, dst_cap[b], pd, ret + b, ax, d);
+#else
     if (tt == kByU32) band_block<kByU32, kSt>(S, im, n, out, dst_cap[b], pd, ret + b, ax, d);
     else if (tt == kByU64) band_block<kByU64, kSt>(S, im, n, out, dst_cap[b], pd, ret + b, ax, d);
     else band_block<kByU16, kSt>(S, im, n, out, dst_cap[b], pd, ret + b, ax, d);
+#endif
 }
 
 }  // namespace
