@@ -57,7 +57,7 @@ namespace lz4e {
 
 namespace {
 
-constexpr int32_t kLong = 64;  // longer literal runs / matches go to the whole wave
+constexpr int32_t kLongPiece = 64;  // longer literal runs / matches go to the whole wave
 
 // LDS per block: the input ring (+ mirror), the store sink, the span buffer.
 constexpr uint32_t kRing = 1024;                    // 4 segments of 256 B
@@ -926,16 +926,16 @@ LZ4E_DEV void copy_scalar_hbm(const Batch& b, const uint8_t* in, int32_t srcSize
     const int32_t ls = lane_val((uint32_t)b.ls, 0);
     const int32_t M = lane_val((uint32_t)b.M, 0), off = lane_val((uint32_t)b.off, 0);
     wave_fence();
-    if (L > 0 && L <= kLong) {
+    if (L > 0 && L <= kLongPiece) {
         if (lane == 0) lane_copy64(gout + op, in + ls, L, in + srcSize);
-    } else if (L > kLong) {
+    } else if (L > kLongPiece) {
         wave_copy<kU>(gout + op, in + ls, L, lane, beat);
     }
     wave_fence();
     const int32_t ms = op + L;
-    if (M > 0 && M <= kLong) {
+    if (M > 0 && M <= kLongPiece) {
         if (lane == 0) lane_match(gout + ms, (uint32_t)off, M, gout + outSize);
-    } else if (M > kLong) {
+    } else if (M > kLongPiece) {
         wave_match(gout, ms, (uint32_t)off, M, lane, beat);
     }
     wave_fence();
@@ -1304,7 +1304,7 @@ LZ4E_DEV void flush_lds(uint8_t* gout, const lu8* obuf, int32_t n, uint32_t lane
     }
 }
 
-struct Stamps {
+struct WaveStamps {
     uint64_t t = 0, acc[4] = {0, 0, 0, 0}, batches = 0, rounds = 0;
 };
 
@@ -1318,7 +1318,7 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
                            int32_t* ret_slot, uint64_t* dbg, uint32_t lane, lu8* span_buf,
                            lu32* ring, lu16* jump, int32_t dict, lu8* sinkb, lu8* obuf = nullptr,
                            lu8* lin = nullptr, int32_t ip0 = 0, int32_t op0 = 0) {
-    Stamps st;
+    WaveStamps st;
     auto lap = [&](int ph) {
         if constexpr (kStamps) {
             const uint64_t now = clock64();
