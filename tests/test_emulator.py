@@ -75,7 +75,10 @@ def _block(kind, n, seed):
 CASES = [("text", 4096, BYU16), ("records", 16384, BYU16), ("ints", 8192, BYU32),
          ("runs", 65536, BYU32), ("random", 20000, BYU32), ("small_alpha", 6000, BYU16),
          ("text", 30000, BYU64), ("text", 12, BYU16), ("text", 13, BYU16), ("text", 0, BYU16),
-         ("records", 32768, BYU16)]
+         ("records", 32768, BYU16),
+         # blocks of <= 4 KiB: staged input, narrow tables (packed byU16, u16 byU32/byU64)
+         ("small_alpha", 4096, BYU16), ("ints", 4096, BYU16), ("runs", 4000, BYU16),
+         ("text", 4096, BYU32), ("ints", 3000, BYU64), ("random", 4096, BYU16)]
 
 
 @pytest.mark.parametrize("kind,n,cls", CASES, ids=[f"{k}-{n}-{c}" for k, n, c in CASES])

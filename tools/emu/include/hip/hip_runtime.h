@@ -181,6 +181,8 @@ inline uint64_t __builtin_amdgcn_s_memtime() { return 0; }
 #define __hip_atomic_load(p, order, scope) __atomic_load_n(p, order)
 #define __hip_atomic_store(p, v, order, scope) __atomic_store_n(p, v, order)
 #define __hip_atomic_fetch_add(p, v, order, scope) __atomic_fetch_add(p, v, order)
+#define __hip_atomic_fetch_and(p, v, order, scope) __atomic_fetch_and(p, v, order)
+#define __hip_atomic_fetch_or(p, v, order, scope) __atomic_fetch_or(p, v, order)
 // LDS atomic max (the dictionary preload): a CAS loop on host memory.
 inline uint32_t atomicMax(uint32_t* p, uint32_t v) {
     uint32_t cur = __atomic_load_n(p, __ATOMIC_RELAXED);

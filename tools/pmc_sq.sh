@@ -7,7 +7,7 @@ tag=${1:-sq}; shift
 for kv in "$@"; do export "$kv"; done
 out=gpurun_out/$tag
 mkdir -p $out
-args=(--steps 1 --warmup 1 --no-cpu-baseline --no-e2e --no-single-call --no-parity --no-strong)
+args=(--steps 1 --warmup 1 --no-cpu-baseline --no-e2e --no-single-call --no-parity --no-strong ${BENCH_ARGS:-})
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS -T -d $out/p1 -o run --output-format csv -- python3 bench.py "${args[@]}" > $out/p1.log 2>&1 || { tail -20 $out/p1.log; exit 1; }
 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_LDS SQ_INSTS_BRANCH -T -d $out/p2 -o run --output-format csv -- python3 bench.py "${args[@]}" > $out/p2.log 2>&1 || { tail -20 $out/p2.log; exit 1; }
 python3 - "$out" <<'PY'
