@@ -638,7 +638,7 @@ int LZ4E_compress_usingDict(const struct bio_vec* src, struct bio_vec* dst, stru
 // 316-336), so no input of csize bytes produces more than 263 * csize.  A
 // caller's capacity beyond that is never touched, and the kernel still sees
 // the caller's capacity (it steers the reference's bound checks).
-uint64_t decode_staging(int csize, int cap) {
+static uint64_t decode_staging(int csize, int cap) {  // internal: not exported
     if (cap <= 0) return 0;
     const uint64_t most = 263ull * (uint64_t)std::max(csize, 0) + 64;
     return std::min<uint64_t>((uint64_t)cap, most);
