@@ -1648,7 +1648,14 @@ __global__ __launch_bounds__(64) void decompress_resume_kernel(
 #endif
 constexpr uint32_t kPipeWaves = LZ4E_PIPE_WAVES;
 constexpr uint32_t kCopiers = kPipeWaves - 1;
-constexpr uint32_t kPipeRecs = 4;
+// LZ4E_PIPE_RECS: record slots between the parser and the copiers (how far
+// the parser may run ahead of the slowest copier; experiments: 6, 8 and 12
+// measured 0.874 / 0.882 / 0.902 ms against 0.878-0.883 ms for 4 on
+// silesia64k, profiles/r05/pipe_recs/).
+#ifndef LZ4E_PIPE_RECS
+#define LZ4E_PIPE_RECS 4
+#endif
+constexpr uint32_t kPipeRecs = LZ4E_PIPE_RECS;
 constexpr uint32_t kPipeSpans = kCopiers + 2;  // see copy_fast's slot safety
 constexpr int32_t kPipeOut = 1024;                   // output bytes per fast batch
 constexpr uint32_t kPipeSpan = kPipeOut + 16 + 48;   // its span (16-B aligned start)
