@@ -208,13 +208,13 @@ int lz4e_compress_batch_dev(const uint8_t *src, const uint64_t *src_off,
  * ret[i] receives LZ4E_decompress_safe's return value.  `max_cap` bounds
  * dst_cap[] (0 = unknown) and selects the decoder: 16-128 KiB (or unknown),
  * and any batch of at most 1024 blocks, the pipelined one (one parser wave
- * and three copier waves per block); <= 4608 bytes the lane decoder for
- * batches of >= 131072 blocks (one block per lane, blocks of short
- * sequences handed to the one-wave decoder), the one-wave decoder's LDS
+ * and three copier waves per block); <= 4608 bytes the group decoder for
+ * batches of >= 16384 blocks (one block per group of 8 lanes, blocks of
+ * short sequences handed to the one-wave decoder), the one-wave decoder's LDS
  * form for 1025-3328 blocks; otherwise one wave per block.  All return identical values and bytes.  Pipelined batches of more
  * than 1536 blocks are launched in decreasing compressed-size order (as for
- * compress, on `stream`).  LZ4E_DECOMPRESS_MODE=w|p|s|l (one-wave,
- * pipelined, LDS form, lane) overrides the choice for experiments.
+ * compress, on `stream`).  LZ4E_DECOMPRESS_MODE=w|p|s|g (one-wave,
+ * pipelined, LDS form, group) overrides the choice for experiments.
  * Returns 0 on a successful launch, else a negative error.
  *
  * ret[i] == LZ4E_DECODE_ABORTED: the pipelined decoder's watchdog fired

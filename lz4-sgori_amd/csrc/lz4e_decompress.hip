@@ -3,8 +3,8 @@
 // Restates /root/reference/lz4e/lz4e_decompress.c:62-469
 // (LZ4E_decompress_generic, instance endOnInputSize + decode_full_block +
 // noDict).  The batch decoders share one parse (parse_batch) and differ in
-// how the copies of a batch are scheduled; the lane decoder runs the scalar
-// loop per lane.  launch_impl picks one per launch ("Auto
+// how the copies of a batch are scheduled; the group decoder runs the scalar
+// loop per group of 8 lanes.  launch_impl picks one per launch ("Auto
 // mode, in full"):
 //
 //  * Parse, in batches of up to 64 sequences: the token stream is walked
@@ -32,10 +32,12 @@
 //    assemble three batches at once, cross-batch sources resolved from the
 //    spans of the two previous batches (see the section below).  19 KiB of
 //    LDS per block.
-//  * decompress_lane_kernel, one block per lane (>= 131072 blocks of <= 4608
-//    bytes), handing blocks of short sequences to decompress_resume_kernel.
+//  * decompress_group_kernel, one block per group of 8 lanes (>= kGroupMinBlocks
+//    blocks of <= 4608 bytes), handing blocks of short sequences to
+//    decompress_resume_kernel.
 //  (The chunked and relay decoders of round 4, never picked by auto mode,
-//  were removed in round 5)
+//  were removed in round 5, and round 4's one-block-per-lane decoder gave way
+//  to the group decoder)
 //
 // Overlapping matches follow LZ semantics out[op + t] = out[op - off + t]
 // byte by byte; offset 0 writes zeros, which is what the reference's
@@ -579,7 +581,7 @@ struct Parse {
 
     // lin (small blocks, srcSize <= kSmallOut): stage the whole block into
     // these kSmallBuf bytes of LDS first, one round trip for all its loads.
-    // (ip0, op0): resume at a sequence boundary (the lane decoder's hand-over)
+    // (ip0, op0): resume at a sequence boundary (the group decoder's hand-over)
     LZ4E_DEV void init(const uint8_t* in, int32_t srcSize, int32_t outSize, lu32* ring,
                        uint32_t lane, int32_t dict = 0, lu8* lin = nullptr, int32_t ip0 = 0,
                        int32_t op0 = 0) {
@@ -941,20 +943,23 @@ LZ4E_DEV void copy_scalar_hbm(const Batch& b, const uint8_t* in, int32_t srcSize
     wave_fence();
 }
 
-// ---------------------------------------------------------------- lane-per-block decoder
+// ---------------------------------------------------------------- block-per-group decoder
 // Large batches of small blocks whose sequences are long (fio-style 4 KiB
 // buffers: ~14 sequences of ~300 bytes) leave the one-wave decoder parsing
 // one scalar sequence at a time with the other 63 lanes idle: ~24 k issue
-// cycles per block (tools/wavestamps.py).  Here every lane decodes a block of
-// its own: the reference's scalar loop (lz4e_decompress.c:123-446, the same
-// checks in the same order as parse_batch's exact path, so values and error
-// codes are the reference's), with 16-byte loads and stores per lane.  A
-// wave then costs about what one of its blocks costs, and a batch of
-// hundreds of thousands of blocks is resident at once.
+// cycles per block (tools/wavestamps.py).  Here a group of kGroup lanes
+// decodes a block of its own (64 / kGroup blocks per wave): the reference's
+// scalar loop (lz4e_decompress.c:123-446, the same checks in the same order
+// as parse_batch's exact path, so values and error codes are the
+// reference's), run by every lane of the group, with each literal run and
+// match copied by the whole group, up to 256 bytes per round.  Round 4's
+// version ran one block per lane with 16-byte copies per lane (fio4k 1.39
+// ms); groups of 8 lanes take 0.88-0.89 ms (groups of 2 / 4 / 16 / 32: 1.10
+// / 0.91 / 0.94 / 1.42 ms, profiles/r05/group_decoder/).
 
 typedef __attribute__((address_space(1))) const uint8_t gcu8;
 LZ4E_DEV uint32_t ldb(const uint8_t* p, int32_t i) { return ((gcu8*)p)[i]; }
-// Global-address-space stores of the lane decoder (flat ones would also
+// Global-address-space stores of the group decoder (flat ones would also
 // count on lgkmcnt and make every wait a wait for both counters).
 typedef __attribute__((address_space(1))) uint64_t gu64w;
 typedef __attribute__((address_space(1))) uint16_t gu16w;
@@ -978,69 +983,6 @@ LZ4E_DEV void gst_tail(uint8_t* p, uint4 c, uint32_t n) {
         lo >>= 16;
     }
     if (n & 1) *(gu8*)p = (uint8_t)lo;
-}
-
-// Per-lane copy of len (1..256) bytes, src + len <= dst or another buffer:
-// every load issued before the first store (one round trip per 256 bytes;
-// the lane decoder runs few waves per CU, so registers are plentiful).
-// Loads never read at or past lim.
-LZ4E_DEV void lane_copy256(uint8_t* dst, const uint8_t* src, int32_t len, const uint8_t* lim) {
-    const uint32_t nch = ((uint32_t)len + 15) >> 4;
-    if (src + 16 * nch > lim) {
-        for (int32_t t = 0; t < len; ++t) *(gu8*)(dst + t) = (uint8_t)ldb(src, t);
-        return;
-    }
-    uint4 c[16];
-#pragma unroll
-    for (uint32_t i = 0; i < 16; ++i) c[i] = i < nch ? ldg16(src + 16 * i) : make_uint4(0, 0, 0, 0);
-    const uint32_t full = (uint32_t)len >> 4, tail = (uint32_t)len & 15;
-#pragma unroll
-    for (uint32_t i = 0; i < 16; ++i) {
-        if (i < full) stg16(dst + 16 * i, c[i]);
-        else if (i == full && tail) gst_tail(dst + 16 * i, c[i], tail);
-    }
-}
-
-// Per-lane copy of len bytes, src + len <= dst or another buffer.
-LZ4E_DEV void lane_copy_any(uint8_t* dst, const uint8_t* src, int32_t len, const uint8_t* lim) {
-    for (int32_t t = 0; t < len; t += 256) lane_copy256(dst + t, src + t, len - t < 256 ? len - t : 256, lim);
-}
-
-// Per-lane match copy out[t] = out[t - off] for t in [0, len), any overlap
-// (offset 0: zeros).  Periods below 16 are first widened from registers
-// (the final period, then whole multiples of it up to >= 16 bytes); then
-// piece [t, t + c) comes from D bytes back, D a multiple of off with
-// c <= D <= t (doubling), so every source byte is written before its piece.
-LZ4E_DEV void lane_match_any(uint8_t* dst, uint32_t off, int32_t len, const uint8_t* lim) {
-    int32_t t = 0;
-    if (off == 0) {
-        for (; t + 16 <= len; t += 16) stg16(dst + t, make_uint4(0, 0, 0, 0));
-        if (t < len) gst_tail(dst + t, make_uint4(0, 0, 0, 0), (uint32_t)(len - t));
-        return;
-    }
-    uint32_t D = off;
-    if (off < 16) {
-        const uint32_t H = off * ((15 + off) / off);  // >= 16, a multiple of off
-        const int32_t h = len < (int32_t)H ? len : (int32_t)H;
-        if (dst - off + 16 > lim) {
-            for (; t < h; ++t) *(gu8*)(dst + t) = (uint8_t)ldb(dst, t - (int32_t)off);
-        } else {
-            const uint4 p = ldg16(dst - off);
-            uint32_t j = 0;
-            for (; t < h; ++t) {
-                *(gu8*)(dst + t) = (uint8_t)pat_byte(p, j);
-                j = (j + 1 == off) ? 0 : j + 1;
-            }
-        }
-        D = H;
-    }
-    while (t < len) {
-        int32_t c = len - t < (int32_t)D ? len - t : (int32_t)D;
-        c = c < 256 ? c : 256;
-        lane_copy256(dst + t, dst + t - D, c, lim);
-        t += c;
-        while (2 * D <= (uint32_t)t) D *= 2;
-    }
 }
 
 // A lane's 16-byte window of its input (token, extension and offset bytes
@@ -1068,16 +1010,13 @@ struct LaneIn {
     }
 };
 
-// One block on one lane: the return value of LZ4E_decompress_safe (D
-// dictionary bytes before out).
-// A lane whose block turns out to hold short sequences (fewer than
+// A group whose block turns out to hold short sequences (fewer than
 // kLaneBailBytes output bytes per sequence over the last kLaneBailSeqs
-// sequences: text, tables) hands the block over at a sequence
-// boundary -- one lane left decoding such a block would hold the whole
-// launch for milliseconds: it
-// returns kLaneHandOver with (*ip_out, *op_out), and the one-wave decoder
-// resumes there (a lane pays a few round trips per sequence, which only
-// long sequences amortise).
+// sequences: text, tables) hands the block over at a sequence boundary --
+// such a block would hold its wave for milliseconds: group_decode returns
+// kLaneHandOver with (*ip_out, *op_out), and the one-wave decoder resumes
+// there (a group pays a few round trips per sequence, which only long
+// sequences amortise).
 constexpr int32_t kLaneHandOver = INT32_MIN;
 #ifndef LZ4E_LANE_BAIL_SEQS
 #define LZ4E_LANE_BAIL_SEQS 4
@@ -1088,8 +1027,118 @@ constexpr int32_t kLaneHandOver = INT32_MIN;
 constexpr int32_t kLaneBailSeqs = LZ4E_LANE_BAIL_SEQS;
 constexpr int32_t kLaneBailBytes = 64;
 constexpr uint32_t kLaneFirstLit = LZ4E_LANE_FIRST_LIT;  // (fio-style: 256)
-LZ4E_DEV int32_t lane_decode(const uint8_t* in, int32_t srcSize, uint8_t* out, int32_t outSize,
-                             int32_t D, bool may_bail, int32_t* ip_out, int32_t* op_out) {
+// A literal run or a match piece of up to 256 bytes leaves in kPer 16-byte
+// loads and stores per lane, contiguous per block.  The group's lanes run the
+// same scalar parse (their input window loads are one address per group).
+// s: the lane's index in its group; dst and src are the group's.
+
+// LZ4E_GROUP: lanes per block (2 .. 16; experiments).
+#ifndef LZ4E_GROUP
+#define LZ4E_GROUP 8
+#endif
+constexpr uint32_t kGroup = LZ4E_GROUP;
+// A round moves up to 256 bytes of a block: kPer 16-byte chunks per lane,
+// every load of the round issued before its first store (loads and stores
+// share one in-order counter, so a load after a store waits for the store).
+constexpr int32_t kRound = 256;
+constexpr uint32_t kPer = kRound / (16 * kGroup);
+static_assert(kPer >= 1 && kPer * 16 * kGroup == kRound, "lanes per block: 1 .. 16, a power of two");
+
+// Literal run: dst[t] = src[t] for t in [0, len), src a different buffer;
+// loads never read at or past lim.
+// 16 bytes at p (n of them wanted), byte by byte where a 16-byte load
+// would reach lim.
+LZ4E_DEV uint4 ld16_lim(const uint8_t* p, uint32_t n, const uint8_t* lim) {
+    if (p + 16 <= lim) return ldg16(p);
+    uint32_t x[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < n; ++k) x[k >> 2] |= ldb(p, (int32_t)k) << (8 * (k & 3));
+    return make_uint4(x[0], x[1], x[2], x[3]);
+}
+LZ4E_DEV void st16_n(uint8_t* p, uint4 v, uint32_t n) {
+    if (n == 16) stg16(p, v);
+    else gst_tail(p, v, n);
+}
+
+LZ4E_DEV void group_copy(uint8_t* dst, const uint8_t* src, int32_t len, const uint8_t* lim, uint32_t s) {
+    for (int32_t t0 = 0; t0 < len; t0 += kRound) {
+        uint4 v[kPer];
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const int32_t q = t0 + 16 * (int32_t)(s + kGroup * i);
+            if (q < len) v[i] = ld16_lim(src + q, (uint32_t)(len - q < 16 ? len - q : 16), lim);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const int32_t q = t0 + 16 * (int32_t)(s + kGroup * i);
+            if (q < len) st16_n(dst + q, v[i], (uint32_t)(len - q < 16 ? len - q : 16));
+        }
+    }
+}
+
+// 16 bytes of the period p (off < 16 bytes, pattern byte j = p's byte j)
+// starting at phase j0.
+LZ4E_DEV uint4 period16(uint4 p, uint32_t off, uint32_t j0) {
+    uint32_t w[4] = {0, 0, 0, 0};
+    uint32_t j = j0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+        w[k >> 2] |= pat_byte(p, j) << (8 * (k & 3));
+        j = (j + 1 == off) ? 0 : j + 1;
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Match: dst[t] = dst[t - off] for t in [0, len), any overlap (offset 0:
+// zeros).  Periods below 16: every lane builds its 16-byte pieces from the
+// period in registers (one pass); otherwise pieces [t, t + c) from D bytes
+// back, D a multiple of off with c <= D <= t (doubling, up to 256 bytes a
+// piece), so every source byte is written before its piece is read (same-wave
+// stores and loads to one address are ordered; group_fence keeps the compiler
+// from moving the loads up).  Loads never read at or past lim.
+LZ4E_DEV void group_match(uint8_t* dst, uint32_t off, int32_t len, const uint8_t* lim, uint32_t s) {
+    if (off == 0 || off < 16) {
+        uint4 p = make_uint4(0, 0, 0, 0);
+        if (off != 0) {
+            if (dst - off + 16 <= lim) {
+                p = ldg16(dst - off);
+            } else {
+                uint32_t x[4] = {0, 0, 0, 0};
+                for (uint32_t k = 0; k < off; ++k) x[k >> 2] |= ldb(dst, (int32_t)k - (int32_t)off) << (8 * (k & 3));
+                p = make_uint4(x[0], x[1], x[2], x[3]);
+            }
+        }
+        for (int32_t t = 16 * (int32_t)s; t < len; t += 16 * (int32_t)kGroup) {
+            const uint32_t n = (uint32_t)(len - t < 16 ? len - t : 16);
+            const uint4 v = off == 0 ? make_uint4(0, 0, 0, 0) : period16(p, off, (uint32_t)t % off);
+            st16_n(dst + t, v, n);
+        }
+        return;
+    }
+    uint32_t D = off;
+    for (int32_t t = 0; t < len;) {
+        int32_t c = len - t < (int32_t)D ? len - t : (int32_t)D;
+        c = c < kRound ? c : kRound;
+        uint4 v[kPer];
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const int32_t q = 16 * (int32_t)(s + kGroup * i);
+            if (q < c) v[i] = ld16_lim(dst + t + q - (int32_t)D, (uint32_t)(c - q < 16 ? c - q : 16), lim);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < kPer; ++i) {
+            const int32_t q = 16 * (int32_t)(s + kGroup * i);
+            if (q < c) st16_n(dst + t + q, v[i], (uint32_t)(c - q < 16 ? c - q : 16));
+        }
+        group_fence(kGroup);
+        t += c;
+        while (2 * D <= (uint32_t)t) D *= 2;
+    }
+}
+
+// One block on one group: the return value of LZ4E_decompress_safe (D
+// dictionary bytes before out), or kLaneHandOver with (*ip_out, *op_out).
+LZ4E_DEV int32_t group_decode(const uint8_t* in, int32_t srcSize, uint8_t* out, int32_t outSize,
+                              int32_t D, bool may_bail, int32_t* ip_out, int32_t* op_out, uint32_t s) {
     const int32_t iend = srcSize, oend = outSize;
     const int32_t shortiend = iend - 14 - 2, shortoend = oend - 14 - 18;  // :100-103
     const uint8_t* ilim = in + srcSize;
@@ -1101,8 +1150,8 @@ LZ4E_DEV int32_t lane_decode(const uint8_t* in, int32_t srcSize, uint8_t* out, i
     I.fill(0);
     if (may_bail) {
         // a block that opens with a short literal run is most likely one of
-        // short sequences: straight to the one-wave decoder
-        // (nor does one whose first match is short: both must be long)
+        // short sequences: straight to the one-wave decoder (nor does one
+        // whose first match is short: both must be long)
         const uint32_t t0 = I.byte(0);
         const uint32_t l0 = (t0 >> 4) == 15 && srcSize > 1 ? 15 + I.byte(1) : t0 >> 4;
         const int32_t q = 2 + (int32_t)l0 + 2;  // the first match's extension byte
@@ -1118,50 +1167,50 @@ LZ4E_DEV int32_t lane_decode(const uint8_t* in, int32_t srcSize, uint8_t* out, i
         if (may_bail && nseq >= kLaneBailSeqs && nseq % kLaneBailSeqs == 0) {
             if (op - op_chk >= kLaneBailBytes * kLaneBailSeqs) {
                 op_chk = op;
-                goto go_on;
+            } else {
+                *ip_out = ip;
+                *op_out = op;
+                return kLaneHandOver;
             }
-            *ip_out = ip;
-            *op_out = op;
-            return kLaneHandOver;
         }
-    go_on:
         const uint32_t token = I.byte(ip);
         ip++;
         uint32_t length = token >> 4;  // saturates at kSat
         int32_t offset;
         if (length != 15 && ip < shortiend && op <= shortoend) {
             // two-stage shortcut (:150-191)
-            if (length) lane_copy256(out + op, in + ip, (int32_t)length, ilim);
+            if (length) group_copy(out + op, in + ip, (int32_t)length, ilim, s);
             op += (int32_t)length;
             ip += (int32_t)length;
             offset = (int32_t)(I.byte(ip) | (I.byte(ip + 1) << 8));
             ip += 2;
             length = token & 15;
             if (length != 15 && offset >= 8 && op >= offset) {
-                lane_match_any(out + op, (uint32_t)offset, (int32_t)length + 4, olim);
+                group_fence(kGroup);
+                group_match(out + op, (uint32_t)offset, (int32_t)length + 4, olim, s);
+                group_fence(kGroup);
                 op += (int32_t)length + 4;
                 continue;
             }
         } else {
             if (length == 15) {  // :194-220
                 if (ip >= iend - 15) break;
-                uint32_t s;
+                uint32_t sb;
                 do {
-                    s = I.byte(ip);
+                    sb = I.byte(ip);
                     ip++;
-                    length = length + s > kSat ? kSat : length + s;
-                } while (ip < iend - 15 && s == 255);
+                    length = length + sb > kSat ? kSat : length + sb;
+                } while (ip < iend - 15 && sb == 255);
             }
             const uint32_t cpy = (uint32_t)op + length;  // :223-288
             const uint32_t iln = (uint32_t)ip + length;
             if (ugt(cpy, oend - 12) || ugt(iln, iend - 8)) {
                 if (iln != (uint32_t)iend || ugt(cpy, oend)) break;
-                lane_copy_any(out + op, in + ip, (int32_t)length, ilim);  // final literal run
+                group_copy(out + op, in + ip, (int32_t)length, ilim, s);  // final literal run
                 return (int32_t)cpy;
             }
-            // the window after the literal run loads under the run's copy
             if ((uint32_t)(ip + (int32_t)length - I.base) + 2 > 16) I.fill(ip + (int32_t)length);
-            lane_copy_any(out + op, in + ip, (int32_t)length, ilim);
+            group_copy(out + op, in + ip, (int32_t)length, ilim, s);
             ip += (int32_t)length;
             op = (int32_t)cpy;
             offset = (int32_t)(I.byte(ip) | (I.byte(ip + 1) << 8));  // :291-296
@@ -1171,21 +1220,23 @@ LZ4E_DEV int32_t lane_decode(const uint8_t* in, int32_t srcSize, uint8_t* out, i
         // _copy_match (:298-336, :422-431)
         if (op - offset + D < 0) break;
         if (length == 15) {
-            uint32_t s;
+            uint32_t sb;
             bool bad = false;
             do {
-                s = I.byte(ip);
+                sb = I.byte(ip);
                 ip++;
                 if (ip > iend - 5) {
                     bad = true;
                     break;
                 }
-                length = length + s > kSat ? kSat : length + s;
-            } while (s == 255);
+                length = length + sb > kSat ? kSat : length + sb;
+            } while (sb == 255);
             if (bad) break;
         }
         if (ugt((uint32_t)op + length + 4, oend - 5)) break;
-        lane_match_any(out + op, (uint32_t)offset, (int32_t)length + 4, olim);
+        group_fence(kGroup);  // the literal run's stores before the match's loads
+        group_match(out + op, (uint32_t)offset, (int32_t)length + 4, olim, s);
+        group_fence(kGroup);
         op += (int32_t)length + 4;
     }
     return -ip - 1;
@@ -1521,65 +1572,54 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
     }
 }
 
-// The lane-per-block decoder (see lane_decode): block b on lane b % 256 of
-// workgroup b / 256.
-#ifndef LZ4E_LANE_WG
-#define LZ4E_LANE_WG 256
+// The block-per-group decoder (see group_decode): block b on group
+// b % (256 / kGroup) of workgroup b / (256 / kGroup).
+constexpr uint32_t kGroupWg = 256;
+// LZ4E_GROUP_PAD: LDS the workgroup never uses (a residency cap; experiments:
+// none is fastest, 4 workgroups per CU cost a third).
+#ifndef LZ4E_GROUP_PAD
+#define LZ4E_GROUP_PAD 0
 #endif
-constexpr uint32_t kLaneWg = LZ4E_LANE_WG;
-// Residency cap: LDS the workgroup never uses, so that one 256-lane
-// workgroup runs per CU.  Fewer blocks in flight keep more of each lane's
-// lines in L2 between its accesses: fio4k 1.46-1.53 -> 1.31-1.38 ms (80 KiB,
-// two per CU: 1.32-1.39).
-#ifndef LZ4E_LANE_PAD
-#define LZ4E_LANE_PAD 163840
-#endif
-__global__ __launch_bounds__(kLaneWg) void decompress_lane_kernel(
+__global__ __launch_bounds__(kGroupWg) void decompress_group_kernel(
     const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off,
     const int32_t* __restrict__ src_len, uint8_t* dst, const uint64_t* __restrict__ dst_off,
     const int32_t* __restrict__ dst_cap, int32_t* __restrict__ ret, uint32_t nblocks,
-    const int32_t* __restrict__ dict_len, uint32_t* __restrict__ handover, uint64_t* __restrict__ dbg) {
-#if LZ4E_LANE_PAD
-    // residency cap (see LZ4E_LANE_PAD)
-    __shared__ uint8_t pad[LZ4E_LANE_PAD];
+    const int32_t* __restrict__ dict_len, uint32_t* __restrict__ handover) {
+#if LZ4E_GROUP_PAD
+    __shared__ uint8_t pad[LZ4E_GROUP_PAD];
     if (nblocks == 0xFFFFFFFFu) ((volatile uint8_t*)pad)[threadIdx.x] = 1;
 #endif
-    const uint32_t b = blockIdx.x * kLaneWg + threadIdx.x, lane = lane_id();
+    const uint32_t tid = threadIdx.x, s = tid % kGroup, lane = lane_id();
+    const uint32_t b = blockIdx.x * (kGroupWg / kGroup) + tid / kGroup;
     // (no lane leaves early: the hand-over below is a whole-wave step)
     bool act = b < nblocks;
     int32_t r = 0, ip = 0, op = 0;
-    const uint64_t t0 = dbg ? clock64() : 0;
     if (act) {
         const int32_t srcSize = src_len[b], outSize = dst_cap[b];
         const uint8_t* in = src + src_off[b];
-        if (special_case(in, srcSize, outSize, ret + b, 0)) act = false;
-        else r = lane_decode(in, srcSize, dst + dst_off[b], outSize, dict_of(dict_len, b), handover != nullptr, &ip, &op);
+        if (special_case(in, srcSize, outSize, ret + b, s)) act = false;
+        else r = group_decode(in, srcSize, dst + dst_off[b], outSize, dict_of(dict_len, b), handover != nullptr,
+                              &ip, &op, s);
     }
-    // hand-over list [count, (block, ip, op) ...] for decompress_resume_kernel:
-    // one atomic per wave (one per lane serialised 65 536 of them on one
-    // address: ~0.3 ms)
+    // hand-over list entries from each group's lane 0, one atomic per wave
     const bool ho = act && r == kLaneHandOver;
-    const uint64_t m = ballot(ho);
+    const uint64_t m = ballot(ho && s == 0);
     if (m) {
         const uint32_t lead = ctz64(m);
         uint32_t base = 0;
         if (lane == lead) base = atomicAdd(handover, popc64(m));
         base = shfl(base, lead);
-        if (ho) {
+        if (ho && s == 0) {
             const uint32_t k = base + popc64(m & ((1ull << lane) - 1));
             handover[1 + 3 * k] = b;
             handover[2 + 3 * k] = (uint32_t)ip;
             handover[3 + 3 * k] = (uint32_t)op;
         }
     }
-    if (act && !ho) ret[b] = r;
-    if (dbg && act) {  // stamped build: the lane's cycles, where it stopped, handed over
-        dbg[8 * (size_t)b + 6] = clock64() - t0;
-        dbg[8 * (size_t)b + 7] = ((uint64_t)(ho ? 1 : 0) << 63) | (uint32_t)op;
-    }
+    if (act && !ho && s == 0) ret[b] = r;
 }
 
-// The blocks the lane decoder handed over, one wave each from their
+// The blocks the group decoder handed over, one wave each from their
 // sequence boundary on (decode_block's HBM form; the output before it is in
 // HBM): workgroup i takes entry i, those past the count leave at once (as
 // balanced as the one-wave kernel itself; a fixed grid striding over the
@@ -2152,13 +2192,14 @@ __global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_MINWG) void decompres
 // profiles/r04/decmodes.txt); at 64 KiB the pipelined decoder's per-block
 // speed wins (silesia64k 0.85 vs 1.20 ms).
 constexpr uint32_t kPipeMinCap = 16384;
-// Batches of at least this many blocks of <= kSmallOut bytes take the lane
+// Batches of at least this many blocks of <= kSmallOut bytes take the group
 // decoder (blocks that open with a short sequence go straight on to the
-// one-wave decoder): a lane's block takes ~1 ms, which only pays once the
-// one-wave decoder needs dozens of rounds of workgroups (fio4k, 262 144
-// blocks: 2.74 -> 1.34-1.39 ms; 4 KiB Silesia-proxy blocks, all handed over:
-// 1.13 -> 1.12 ms; tools/decmodes.py).
-constexpr uint32_t kLaneMinBlocks = 131072;
+// one-wave decoder).  Fio-style blocks (tools/decmodes.py, group vs one-wave
+// vs LDS form): 4 096 blocks 0.080 / 0.055 / 0.067 ms, 16 384 0.093 / 0.170 /
+// 0.189, 65 536 0.279 / 0.717 / 0.693, 262 144 0.89 / 2.76 / 2.69; 4 KiB
+// Silesia-proxy blocks, all handed over: 65 536 1.215 / 1.131 / 1.316
+// (profiles/r05/group_decoder/).
+constexpr uint32_t kGroupMinBlocks = 16384;
 // Batches of small blocks that fit one round of the LDS form's workgroups
 // (11.8 KiB of LDS: 13 per CU) take that form: no HBM round trip inside a
 // block's decode (drop-in single call, 4 KiB text: 89 -> 79 us p50); with
@@ -2195,10 +2236,10 @@ struct DecodeWeight {
 template <bool kStamps>
 hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* dbg) {
     if (a.nblocks == 0) return hipSuccess;
-    // LZ4E_DECOMPRESS_MODE=w|p|s|l (one-wave, pipelined, LDS form, lane)
+    // LZ4E_DECOMPRESS_MODE=w|p|s|g (one-wave, pipelined, LDS form, group)
     // overrides the choice for A/B experiments; any other value is auto.
     // Auto, in order: capacity 16-128 KiB (or unknown) -> pipelined; blocks
-    // of <= kSmallOut bytes in batches of >= kLaneMinBlocks -> lane; batches
+    // of <= kSmallOut bytes in batches of >= kGroupMinBlocks -> group; batches
     // of <= kLatencyMaxBlocks blocks of any size -> pipelined; blocks of
     // <= kSmallOut bytes in batches of <= kSmallMaxBlocks -> LDS form;
     // everything else -> one wave per block.
@@ -2208,13 +2249,13 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
         mode = env[0] == 'w'   ? kDecWave
                : env[0] == 'p' ? kDecPipe
                : env[0] == 's' ? kDecSmall
-               : env[0] == 'l' ? kDecLane
+               : env[0] == 'g' ? kDecGroup
                                : kDecAuto;
     if (mode == kDecAuto)
         mode = (a.max_cap == 0 || (a.max_cap >= kPipeMinCap && a.max_cap < kPipeMaxCap))
                    ? kDecPipe
-                   : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks >= kLaneMinBlocks
-                          ? kDecLane
+                   : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks >= kGroupMinBlocks
+                          ? kDecGroup
                           : (a.nblocks <= kLatencyMaxBlocks
                                  ? kDecPipe
                                  : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks <= kSmallMaxBlocks ? kDecSmall
@@ -2237,7 +2278,7 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
         if (order) (void)hipFreeAsync(order, stream);
         return err;
     }
-    if (mode == kDecLane) {
+    if (mode == kDecGroup) {
         // hand-over list (count + 3 words per block); without it every lane
         // decodes its block to the end
         uint32_t* ho = nullptr;
@@ -2247,9 +2288,9 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
             if (ho) (void)hipFreeAsync(ho, stream);
             ho = nullptr;
         }
-        hipLaunchKernelGGL(decompress_lane_kernel, dim3((a.nblocks + kLaneWg - 1) / kLaneWg), dim3(kLaneWg), 0,
-                           stream, a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks,
-                           a.dict_len, ho, dbg);
+        hipLaunchKernelGGL(decompress_group_kernel, dim3((a.nblocks + kGroupWg / kGroup - 1) / (kGroupWg / kGroup)),
+                           dim3(kGroupWg), 0, stream, a.src, a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap,
+                           a.ret, a.nblocks, a.dict_len, ho);
         hipError_t err = hipGetLastError();
         if (ho) {
             if (err == hipSuccess) {

@@ -881,7 +881,7 @@ int lz4e_debug_decompress_stamped(const uint8_t* src, const uint64_t* src_off, c
                                   int32_t* ret, uint32_t nblocks, void* stream, uint64_t* dbg,
                                   uint32_t max_cap, uint32_t mode) {
     if (mode != lz4e::kDecAuto && mode != lz4e::kDecWave && mode != lz4e::kDecPipe && mode != lz4e::kDecSmall &&
-        mode != lz4e::kDecLane)
+        mode != lz4e::kDecGroup)
         return -1;
     lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap, mode};
     const hipStream_t s = static_cast<hipStream_t>(stream);

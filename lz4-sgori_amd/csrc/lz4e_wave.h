@@ -155,6 +155,10 @@ LZ4E_DEV uint64_t clock64() { return __builtin_amdgcn_s_memtime(); }
 #ifndef LZ4E_EMU
 // Order this wave's LDS/global accesses (memory model fence, wavefront scope).
 LZ4E_DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+// wave_fence for code run by groups of `width` lanes that diverge from each
+// other (the group decoder): the same fence on the GPU, a barrier of the
+// group's lanes in the emulator.
+LZ4E_DEV void group_fence(uint32_t) { wave_fence(); }
 // The lanes of a wave execute in lockstep: a memory instruction completes
 // (LDS) or is ordered (global stores to one address) for every lane before
 // the wave's next one.  Marks the places that rely on it -- a whole-wave put
@@ -180,6 +184,7 @@ LZ4E_DEV uint32_t vaddr(uint32_t q) {
 // lockstep execution is a barrier of the emulated wave; the workgroup
 // barrier is the emulated workgroup's.
 LZ4E_DEV void wave_fence() { emu_wave_barrier(); }
+LZ4E_DEV void group_fence(uint32_t width) { emu_group_barrier(width); }
 LZ4E_DEV void lockstep() { emu_wave_barrier(); }
 LZ4E_DEV void block_sync() { __syncthreads(); }
 LZ4E_DEV void stores_done() { __atomic_thread_fence(__ATOMIC_SEQ_CST); }

@@ -220,7 +220,8 @@ LANE_CASES = [(k, m) for k in ("text", "fio", "random", "head") for m in range(5
 
 @pytest.mark.parametrize("kind,mode", LANE_CASES, ids=[f"{k}-{m}" for k, m in LANE_CASES])
 def test_emulated_lane_decoder_sanitized(emu_exe, tmp_path, kind, mode):
-    """The lane-per-block decoder (one block per lane) and its hand-over to
+    """The block-per-group decoder (one block per 8-lane group, copies over
+    the group) and its hand-over to
     the one-wave decoder: blocks that open with a short literal run go over
     at once (text), long-sequence blocks stay on their lane (fio, random),
     and "head" blocks (230 random bytes, 200 zeros, then text) go over
@@ -250,7 +251,7 @@ def test_emulated_lane_decoder_sanitized(emu_exe, tmp_path, kind, mode):
         elif mode == 3:
             cap = max(0, len(blk) - int(rng.integers(1, 40)))
         want = oracle_ref.decompress_dict(f, cap, dic)
-        got = _emu_decode(emu_exe, tmp_path, f, cap, dic, "-n")
+        got = _emu_decode(emu_exe, tmp_path, f, cap, dic, "-g")
         assert got[0] == want[0], (rep, got[0], want[0])
         if want[0] >= 0:
             assert got[1] == want[1], rep

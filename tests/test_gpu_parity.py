@@ -72,7 +72,7 @@ def _gpu_compress(amd, blocks, ttypes, caps=None):
     return r, frames, ax
 
 
-DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_SMALL, DEC_LANE = 0, 1, 2, 6, 7
+DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_SMALL, DEC_GROUP = 0, 1, 2, 6, 7
 
 
 def _gpu_decompress(amd, frames, caps, csizes=None, max_cap=None, mode=DEC_AUTO):
@@ -276,8 +276,8 @@ def test_decompress_batch_vs_oracle(gpu, kind):
         assert outs[i] == eo == expect[i]
 
 
-@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_PIPE, DEC_WAVE, DEC_SMALL, DEC_LANE],
-                         ids=["auto", "pipe", "wave", "small", "lane"])
+@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_PIPE, DEC_WAVE, DEC_SMALL, DEC_GROUP],
+                         ids=["auto", "pipe", "wave", "small", "group"])
 @pytest.mark.parametrize("mode", ["truncate", "flip", "garbage", "small_cap", "csize"])
 def test_decompress_error_codes(gpu, mode, dec):
     rng = np.random.default_rng(1234 + len(mode))
@@ -350,7 +350,7 @@ def test_decompress_small_blocks_in_lds(gpu, kind):
         frames.append(f)
         caps.append(cap)
         want.append(oracle_ref.decompress(f, cap))
-    for mode in (DEC_AUTO, DEC_SMALL, DEC_LANE):
+    for mode in (DEC_AUTO, DEC_SMALL, DEC_GROUP):
         r, outs = _gpu_decompress(gpu, frames, caps, max_cap=max(caps), mode=mode)
         for i, (er, eb) in enumerate(want):
             assert r[i] == er, (mode, i, r[i], er)
@@ -744,7 +744,7 @@ def test_full_size_sg512_layout_every_frame(gpu):
 @pytest.mark.parametrize("kind", ["mixed", "text", "runs", "ints", "random", "small_alpha", "fio"])
 def test_decompress_pipelined_vs_wave_decoder(gpu, kind):
     """The four decoders on the same frames -- the pipelined 4-wave decoder,
-    the one-wave decoder, its LDS form and the lane decoder -- valid frames,
+    the one-wave decoder, its LDS form and the group decoder -- valid frames,
     exact and spare capacities, and corrupted ones: identical values and
     bytes, all equal to the oracle's."""
     rng = np.random.default_rng(zlib.crc32(kind.encode()))
@@ -774,12 +774,12 @@ def test_decompress_pipelined_vs_wave_decoder(gpu, kind):
     r_wg, o_wg = _gpu_decompress(gpu, frames, caps, mode=DEC_PIPE)
     r_wv, o_wv = _gpu_decompress(gpu, frames, caps, mode=DEC_WAVE)
     r_sm, o_sm = _gpu_decompress(gpu, frames, caps, mode=DEC_SMALL)
-    r_ln, o_ln = _gpu_decompress(gpu, frames, caps, mode=DEC_LANE)
+    r_gp, o_gp = _gpu_decompress(gpu, frames, caps, mode=DEC_GROUP)
     for i, (er, eb) in enumerate(want):
-        assert r_wg[i] == er == r_wv[i] == r_sm[i] == r_ln[i], \
-            (i, r_wg[i], er, r_wv[i], r_sm[i], r_ln[i])
+        assert r_wg[i] == er == r_wv[i] == r_sm[i] == r_gp[i], \
+            (i, r_wg[i], er, r_wv[i], r_sm[i], r_gp[i])
         if er >= 0:
-            assert o_wg[i] == eb == o_wv[i] == o_sm[i] == o_ln[i], i
+            assert o_wg[i] == eb == o_wv[i] == o_sm[i] == o_gp[i], i
 
 
 # ---------------------------------------------------------------------------

@@ -21,7 +21,7 @@ L = lz4e_amd.lib()
 P = ctypes.c_void_p
 L.lz4e_debug_decompress_stamped.argtypes = [P] * 7 + [ctypes.c_uint32, P, P, ctypes.c_uint32,
                                                        ctypes.c_uint32]
-NAMES = {1: "one-wave", 2: "pipelined", 6: "lds-small", 7: "lane"}
+NAMES = {1: "one-wave", 2: "pipelined", 6: "lds-small", 7: "group"}
 
 
 def class_blocks(kind, n, bs):
@@ -99,5 +99,8 @@ if __name__ == "__main__":
         run("fio4k_1k", corpus.fio_pattern(1024 * 4096), 4096, 1, modes)
     if "sil4k_3k" in wls:
         run("sil4k_3k", corpus.silesia_proxy(3072 * 4096, 0x5157), 4096, 1, modes)
+    for nb in (4096, 16384, 65536):  # fio blocks in mid-size batches (lane / group thresholds)
+        if f"fio4k_{nb // 1024}k" in wls:
+            run(f"fio4k_{nb // 1024}k", corpus.fio_pattern(nb * 4096), 4096, 1, modes)
     if "sil4k" in wls:  # short sequences in small blocks
         run("sil4k", corpus.silesia_proxy(65536 * 4096, 0x5157), 4096, 1, modes)

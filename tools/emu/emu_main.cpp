@@ -5,8 +5,8 @@
 //            4 waves: parser + 3 copiers)
 //   emu_main -l FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (one-wave decoder,
 //            LDS output for blocks of <= 4608 bytes without a dictionary)
-//   emu_main -n FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (lane-per-block
-//            decoder)
+//   emu_main -g FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (block-per-group
+//            decoder, 8 lanes a block)
 // compresses one block through the unmodified kernel source, prints the
 // return value and the iterator post-state words, and writes the frame.
 // With DICT_FILE the block is compressed in dictionary mode against the
@@ -61,9 +61,9 @@ static int decode_main(int argc, char** argv) {
     // the decoder reads the input window by aligned dwords (the GPU's word
     // granularity: the dword holding the last byte); the heap block covers it
     frame.reserve((frame.size() + 3) & ~(size_t)3);
-    // kDecPipe / kDecSmall / kDecLane / kDecWave
+    // kDecPipe / kDecSmall / kDecGroup / kDecWave
     const char m = argv[1][1];
-    const uint32_t mode = m == 'p' ? 2u : (m == 'l' ? 6u : (m == 'n' ? 7u : 1u));
+    const uint32_t mode = m == 'p' ? 2u : (m == 'l' ? 6u : (m == 'g' ? 7u : 1u));
     emu_decompress_batch_mode(frame.data(), &so, &csize, out.data(), &doff, &cap, &ret, 1, &D, mode);
     char err[256];
     const int good = emu_decode_results(&ret, 1, err, sizeof err);
@@ -79,7 +79,7 @@ static int decode_main(int argc, char** argv) {
 
 int main(int argc, char** argv) {
     if (argc > 3 && argv[1][0] == '-' &&
-        (argv[1][1] == 'd' || argv[1][1] == 'p' || argv[1][1] == 'l' || argv[1][1] == 'n'))
+        (argv[1][1] == 'd' || argv[1][1] == 'p' || argv[1][1] == 'l' || argv[1][1] == 'g'))
         return decode_main(argc, argv);
     if (argc < 3) {
         fprintf(stderr, "usage: emu_main BLOCK_FILE TABLE_CLASS [FRAME_OUT]\n");

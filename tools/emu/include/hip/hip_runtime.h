@@ -17,6 +17,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <barrier>
+#include <deque>
 #include <functional>
 #include <thread>
 
@@ -61,7 +62,19 @@ inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) {
 // ---- emulated wave / workgroup --------------------------------------------
 struct EmuWave {
     std::barrier<> bar{64};
+    // barriers of the wave's lane groups of 2, 4, 8, 16 and 32 lanes
+    // (group_fence): 32 + 16 + 8 + 4 + 2 of them, by width
+    std::deque<std::barrier<>> groups;
     uint64_t slot[64];
+    EmuWave() {
+        for (uint32_t w = 2; w <= 32; w *= 2)
+            for (uint32_t g = 0; g < 64 / w; ++g) groups.emplace_back(w);
+    }
+    std::barrier<>& group_bar(uint32_t width, uint32_t lane) {
+        uint32_t base = 0;
+        for (uint32_t w = 2; w < width; w *= 2) base += 64 / w;
+        return groups[base + lane / width];
+    }
 };
 extern thread_local EmuWave* g_emu_wave;
 extern thread_local uint32_t g_emu_lane;
@@ -70,6 +83,7 @@ extern dim3 blockIdx, gridDim;
 extern thread_local dim3 threadIdx;
 
 inline void emu_wave_barrier() { g_emu_wave->bar.arrive_and_wait(); }
+inline void emu_group_barrier(uint32_t width) { g_emu_wave->group_bar(width, g_emu_lane & 63).arrive_and_wait(); }
 // Every lane publishes v; lane l reads the value of lane from(l).
 inline uint64_t emu_gather(uint64_t v, uint32_t from) {
     g_emu_wave->slot[g_emu_lane] = v;

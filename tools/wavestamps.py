@@ -49,15 +49,8 @@ def run(name, data, bs, cls, modes):
             torch.cuda.synchronize()
         assert torch.equal(out[:n * bs], src) and bool((dret == lens).all().item())
         d = dbg.view(n, 8).cpu().numpy().astype(np.float64)
-        if mode == 7:  # lane decoder: the lane pass's cycles per block, hand-overs
-            raw = dbg.view(n, 8).cpu().numpy()
-            cyc = raw[:, 6].astype(np.float64)
-            ho = (raw[:, 7].astype(np.uint64) >> np.uint64(63)).astype(bool)
-            opv = (raw[:, 7].astype(np.uint64) & np.uint64(0xFFFFFFFF)).astype(np.int64)
-            print(f"== {name} lane pass: cycles/lane mean {cyc.mean():.0f} p50 {np.median(cyc):.0f} "
-                  f"p99 {np.percentile(cyc, 99):.0f} max {cyc.max():.0f}; handed over {ho.mean():.3f} "
-                  f"(at op 0: {(ho & (opv == 0)).mean():.3f}); max-cycle lane op {opv[np.argmax(cyc)]}, "
-                  f"handed over {bool(ho[np.argmax(cyc)])}", flush=True)
+        if mode == 7:  # group decoder: no per-block stamps (only the resumed blocks' one-wave stamps)
+            print(f"== {name} mode 7 (group decoder): handed-over blocks' one-wave stamps only", flush=True)
         tot = d[:, 0] + d[:, 1] + d[:, 2] + d[:, 5]
         print(f"== {name} mode {mode}: cycles/block mean {tot.mean():.0f} (p90 {np.percentile(tot, 90):.0f}): "
               f"parse {d[:, 0].mean():.0f}, loads+span {d[:, 1].mean():.0f}, copies/rounds {d[:, 2].mean():.0f}, "
