@@ -32,7 +32,7 @@ def main():
     res = json.load(open(out)) if os.path.exists(out) else {}
     ent = {}
     for k, d in (("compress_kernel", "compress"), ("decompress_pipe_kernel", "decompress"),
-                 ("decompress_kernel", "decompress")):
+                 ("decompress_group_kernel", "decompress"), ("decompress_kernel", "decompress")):
         name = next((n for n in fetch if n.startswith(k)), None)
         if name is None or d in ent:
             continue
