@@ -17,6 +17,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <barrier>
+#include <chrono>
 #include <deque>
 #include <functional>
 #include <thread>
@@ -188,7 +189,16 @@ inline int __shfl_up(int v, unsigned d) {
 }
 inline uint64_t __builtin_amdgcn_s_memtime() { return 0; }
 #define __builtin_amdgcn_s_setprio(x) ((void)0)
-#define __builtin_amdgcn_s_sleep(x) std::this_thread::yield()
+// s_sleep (only in the decoders' wave-uniform wait loops): the wave's lanes
+// meet, lane 0 sleeps 20 us, the others block in the barrier -- a waiting
+// wave then holds no CPU, where 64 yielding threads per wave starved the
+// wave they waited for (a 4-wave workgroup is 256 host threads).
+inline void emu_sleep() {
+    emu_wave_barrier();
+    if ((g_emu_lane & 63) == 0) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    emu_wave_barrier();
+}
+#define __builtin_amdgcn_s_sleep(x) emu_sleep()
 
 // ---- atomics --------------------------------------------------------------
 #define __HIP_MEMORY_SCOPE_WORKGROUP 0
