@@ -1573,8 +1573,14 @@ __global__ __launch_bounds__(64) void decompress_kernel(const uint8_t* __restric
 }
 
 // The block-per-group decoder (see group_decode): block b on group
-// b % (256 / kGroup) of workgroup b / (256 / kGroup).
-constexpr uint32_t kGroupWg = 256;
+// b % (kGroupWg / kGroup) of workgroup b / (kGroupWg / kGroup).
+// LZ4E_GROUP_WG: threads per workgroup (experiments: one wave per workgroup
+// is fastest, fio4k 0.836 ms against 0.850 / 0.892 / 0.988 / 1.012 ms for
+// 128 / 256 / 512 / 1024 threads, profiles/r05/group_decoder/wg/).
+#ifndef LZ4E_GROUP_WG
+#define LZ4E_GROUP_WG 64
+#endif
+constexpr uint32_t kGroupWg = LZ4E_GROUP_WG;
 // LZ4E_GROUP_PAD: LDS the workgroup never uses (a residency cap; experiments:
 // none is fastest, 4 workgroups per CU cost a third).
 #ifndef LZ4E_GROUP_PAD
