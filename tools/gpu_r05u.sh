@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 5: group decoder workgroup size variants on fio4k.
-o=gpurun_out/r05u; mkdir -p $o
+o=gpurun_out/${1:-r05u}; mkdir -p $o
 export TMPDIR=/tmp
 timeout -k 10 300 python -u tools/decmodes.py 7 fio4k,fio4k_16k > $o/decmodes_lib.txt 2>&1 || { cat $o/decmodes_lib.txt; exit 1; }
 grep "==" $o/decmodes_lib.txt | cut -c1-200
