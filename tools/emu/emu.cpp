@@ -24,7 +24,7 @@ int launch_order_mode(bool) { return kOrderNever; }
 
 thread_local EmuWave* g_emu_wave;
 thread_local uint32_t g_emu_lane;
-thread_local std::barrier<>* g_emu_group;
+thread_local EmuBarrier* g_emu_group;
 dim3 blockIdx, gridDim;
 thread_local dim3 threadIdx;
 
@@ -34,7 +34,7 @@ void emu_launch(uint32_t nblocks, uint32_t threads, std::function<void()> body) 
     for (uint32_t b = 0; b < nblocks; ++b) {
         blockIdx = dim3(b);
         std::unique_ptr<EmuWave[]> waves(new EmuWave[nw]);
-        std::barrier<> group((std::ptrdiff_t)(64 * nw));
+        EmuBarrier group((std::ptrdiff_t)(64 * nw));
         memset(lz4e::smem, 0xA5, sizeof(lz4e::smem));  // LDS is not zeroed on the GPU
         std::vector<std::thread> th;
         for (uint32_t t = 0; t < 64 * nw; ++t)

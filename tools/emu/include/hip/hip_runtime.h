@@ -17,6 +17,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <barrier>
+#include <condition_variable>
+#include <mutex>
 #include <chrono>
 #include <deque>
 #include <functional>
@@ -61,17 +63,42 @@ inline hipError_t hipMemsetAsync(void* p, int v, size_t n, hipStream_t) {
 }
 
 // ---- emulated wave / workgroup --------------------------------------------
+// A barrier whose waiters block at once (mutex + condition variable):
+// std::barrier's waiters spin before they sleep, and with every lane a host
+// thread (256 per 4-wave workgroup) the spinning starved the lanes still to
+// arrive -- the pipelined decoder's emulation then ran for minutes.
+class EmuBarrier {
+  public:
+    explicit EmuBarrier(std::ptrdiff_t n) : n_(n) {}
+    void arrive_and_wait() {
+        std::unique_lock<std::mutex> lk(m_);
+        const uint64_t gen = gen_;
+        if (++count_ == n_) {
+            count_ = 0;
+            ++gen_;
+            cv_.notify_all();
+            return;
+        }
+        cv_.wait(lk, [&] { return gen_ != gen; });
+    }
+
+  private:
+    std::mutex m_;
+    std::condition_variable cv_;
+    std::ptrdiff_t n_, count_ = 0;
+    uint64_t gen_ = 0;
+};
 struct EmuWave {
-    std::barrier<> bar{64};
+    EmuBarrier bar{64};
     // barriers of the wave's lane groups of 2, 4, 8, 16 and 32 lanes
     // (group_fence): 32 + 16 + 8 + 4 + 2 of them, by width
-    std::deque<std::barrier<>> groups;
+    std::deque<EmuBarrier> groups;
     uint64_t slot[64];
     EmuWave() {
         for (uint32_t w = 2; w <= 32; w *= 2)
             for (uint32_t g = 0; g < 64 / w; ++g) groups.emplace_back(w);
     }
-    std::barrier<>& group_bar(uint32_t width, uint32_t lane) {
+    EmuBarrier& group_bar(uint32_t width, uint32_t lane) {
         uint32_t base = 0;
         for (uint32_t w = 2; w < width; w *= 2) base += 64 / w;
         return groups[base + lane / width];
@@ -79,7 +106,7 @@ struct EmuWave {
 };
 extern thread_local EmuWave* g_emu_wave;
 extern thread_local uint32_t g_emu_lane;
-extern thread_local std::barrier<>* g_emu_group;
+extern thread_local EmuBarrier* g_emu_group;
 extern dim3 blockIdx, gridDim;
 extern thread_local dim3 threadIdx;
 
