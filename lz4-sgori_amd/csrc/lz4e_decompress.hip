@@ -2189,818 +2189,6 @@ __global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_MINWG) void decompres
     }
 }
 
-// ============================================================================
-// Wide decoder: one 256-thread workgroup per block, token starts found ahead
-// ============================================================================
-//
-// The batch decoders above parse a block's token stream as a chain of 64-
-// sequence batches, one wave at a time: the parse is the block's critical
-// path (~4 k cycles per batch of ~256 compressed bytes).  Here the token
-// starts are found for every block at once before the decode, and a block's
-// decode is a loop over its compressed bytes in chunks of 2 KiB, every step
-// of which is spread over the whole workgroup:
-//
-//  * decompress_walk_kernel: one thread per 32-byte segment of a block's
-//    compressed bytes.  A walker takes the byte kWWarm bytes before its
-//    segment as a token and follows the token chain (next = token + 1 +
-//    literal-length bytes + literals + 2 + match-length bytes) through the
-//    segment; it records the positions it visits inside the segment (one
-//    bit per byte) and where the chain leaves the segment.  A chain started
-//    at a wrong position joins the true chain at the first true token it
-//    lands on, and from there on it *is* the true chain, so the walkers'
-//    marks are the block's token starts wherever the true chain meets a
-//    walker that has joined it -- which the decode checks (a hint: a wrong
-//    one costs time, never a result).
-//  * decompress_wide_kernel, per chunk (the 64 segments from the true token
-//    ip on): wave 0 follows the walkers' exits from ip by pointer doubling
-//    over the 64 segments (segment -> the segment where its chain goes on),
-//    checks that each segment on the path was entered at a position its
-//    walker marked (else re-walks that segment from the true entry), and
-//    lists the chunk's token starts.  Every thread then decodes three
-//    tokens' fields from the chunk staged in LDS, a workgroup scan gives
-//    each sequence its output position, and each sequence is checked
-//    against the reference's conditions (lz4e_decompress.c:123-446) for
-//    its (ip, op): the first one the reference would not take as a normal
-//    sequence (the last literals, an error, a header past the staged
-//    bytes) ends the chunk there.  The chunk's output is then assembled in
-//    4 KiB steps, 16 bytes per thread: each byte is a literal (from the
-//    staged chunk), a match byte whose source lies before the step (final
-//    in HBM: loaded), or one whose source lies in the step (a pointer,
-//    resolved by pointer jumping); a self-overlapping match points into its
-//    first period, so runs are not chains.  One pass of 16-byte stores.
-//  * the sequence that ended the chunk, if any, goes through the
-//    reference's loop for one sequence (wide_exact_seq: the same checks in
-//    the same order as parse_batch's exact path, copies shared by the
-//    workgroup): that decides the last literal run, every error value, and
-//    long literal runs whose header does not fit the staged chunk.
-//
-// The walkers' marks and exits live in HBM scratch (8 bytes per 32
-// compressed bytes); a block whose compressed size exceeds what the launch
-// sized the scratch for is decoded by wide_exact_seq alone.
-
-constexpr uint32_t kWSeg = 32;                        // compressed bytes per walker segment
-constexpr int32_t kWWarm = 96;                        // bytes a walker walks before its segment
-constexpr uint32_t kWThreads = 256;                   // walk and wide workgroups
-constexpr uint32_t kWalkSpan = kWThreads * kWSeg;     // compressed bytes per walk workgroup
-constexpr uint32_t kWalkStage = kWWarm + kWalkSpan + 64;
-constexpr uint32_t kWChunk = 64 * kWSeg;              // compressed bytes whose tokens a chunk lists
-constexpr int32_t kWStage = kWChunk + 256;            // staged bytes (headers may run past the chunk)
-constexpr uint32_t kWMaxTok = kWChunk / 3 + 5;        // tokens start >= 3 bytes apart
-constexpr uint32_t kWPer = 3;                         // tokens per thread in the field pass
-static_assert(kWPer * kWThreads >= kWMaxTok, "field pass covers the chunk");
-constexpr uint32_t kWGroups = 2;                      // 16-byte groups per thread in a step
-constexpr uint32_t kWGroup = 16 * kWThreads;          // output bytes of one group of every thread
-constexpr int32_t kWStep = kWGroups * kWGroup;        // output bytes per assembly step
-constexpr uint16_t kWFinal = 0x8000;                  // entry: final byte (low 8 bits)
-constexpr int32_t kWMore = INT32_MIN + 1;             // wide_exact_seq: block not finished
-
-struct WideLds {
-    uint8_t stage[kWStage + 16];
-    uint32_t rec[kWMaxTok][3];  // op, lit | L << 16, off (the token's position until the fields pass)
-    uint16_t ent[kWStep];
-    int32_t wsum[kWThreads / kWave];
-    uint32_t bad;      // (first sequence the chunk cannot take) << 1 | deferred
-    int32_t more[3];   // pointer-jumping round flags (rotating)
-    int32_t ntok, opE, next_ip;
-};
-
-// Token chain step of a walker: the position after the sequence whose token
-// is at p, read with rb (0 past n).  The reference's own reads of the same
-// bytes (lz4e_decompress.c:125-127, 194-206, 291-296, 316-326).
-template <class RB>
-LZ4E_DEV int32_t walk_next(RB rb, int32_t n, int32_t p) {
-    const uint32_t t = rb(p);
-    int32_t q = p + 1;
-    int32_t L = (int32_t)(t >> 4);
-    if (L == 15) {
-        uint32_t s;
-        do {
-            s = rb(q);
-            q++;
-            L += (int32_t)s;
-        } while (s == 255 && q < n);
-    }
-    q = L > n ? n + 2 : q + L + 2;  // (a run past the block ends the chain)
-    if ((t & 15) == 15) {
-        uint32_t s;
-        do {
-            s = rb(q);
-            q++;
-        } while (s == 255 && q < n);
-    }
-    return q;
-}
-
-// The chain from start through segment [s0, s0 + 32): marks of the positions
-// it visits inside, and the first position at or past the segment's end (or
-// past n: the chain ended).
-template <class RB>
-LZ4E_DEV void walk_segment(RB rb, int32_t n, int32_t s0, int32_t start, uint32_t& marks, int32_t& exit) {
-    const int32_t s1 = s0 + (int32_t)kWSeg;
-    int32_t p = start;
-    uint32_t m = 0;
-    while (p < s1 && p < n) {
-        if (p >= s0) m |= 1u << (p - s0);
-        p = walk_next(rb, n, p);
-    }
-    marks = m;
-    exit = p;
-}
-
-// Walkers: workgroup w of block b covers segments [256 w, 256 w + 256) of
-// its compressed bytes; marks / exits of segment s at b * spb + s.
-__global__ __launch_bounds__(kWThreads) void decompress_walk_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off, const int32_t* __restrict__ src_len,
-    uint32_t nblocks, uint32_t wg_per_block, uint32_t spb, uint32_t* __restrict__ marks,
-    int32_t* __restrict__ exits) {
-    __shared__ __attribute__((aligned(16))) uint8_t stg[kWalkStage];
-    const uint32_t b = blockIdx.x / wg_per_block, w = blockIdx.x % wg_per_block;
-    if (b >= nblocks) return;
-    const int32_t n = src_len[b];
-    const int32_t base = (int32_t)(w * kWalkSpan);
-    if (n <= 0 || (int64_t)n > (int64_t)spb * kWSeg || base >= n) return;
-    const uint8_t* in = src + src_off[b];
-    const uint32_t t = threadIdx.x;
-    // stage block bytes [lo, lo + kWalkStage), 0 outside [0, n)
-    const int32_t lo = base - kWWarm;
-    for (uint32_t i = t; i < kWalkStage / 16; i += kWThreads) {
-        const int32_t q = lo + 16 * (int32_t)i;
-        uint4 v;
-        if (q >= 0 && q + 16 <= n) {
-            v = ldg16(in + q);
-        } else {
-            uint32_t x[4] = {0, 0, 0, 0};
-            for (int32_t k = 0; k < 16; ++k)
-                if (q + k >= 0 && q + k < n) x[k >> 2] |= ldb(in, q + k) << (8 * (k & 3));
-            v = make_uint4(x[0], x[1], x[2], x[3]);
-        }
-        *(uint4*)(stg + 16 * i) = v;
-    }
-    __syncthreads();
-    const int32_t s0 = base + (int32_t)(t * kWSeg);
-    if (s0 >= n) return;
-    auto rb = [&](int32_t q) -> uint32_t {
-        const uint32_t r = (uint32_t)(q - lo);
-        if (r < kWalkStage) return stg[r];
-        return q < n ? ldb(in, q) : 0u;
-    };
-    uint32_t m;
-    int32_t x;
-    walk_segment(rb, n, s0, s0 - kWWarm < 0 ? 0 : s0 - kWWarm, m, x);
-    const size_t i = (size_t)b * spb + (size_t)(s0 / (int32_t)kWSeg);
-    marks[i] = m;
-    exits[i] = x;
-}
-
-// Stage block bytes [p0, p0 + kWStage) into LDS (0 past iend), every thread.
-LZ4E_DEV void wide_stage(uint8_t* stage, const uint8_t* in, int32_t iend, int32_t p0, uint32_t tid) {
-    for (int32_t i = (int32_t)tid; i < (kWStage + 15) / 16; i += (int32_t)kWThreads) {
-        const int32_t q = p0 + 16 * i;
-        uint4 v;
-        if (q + 16 <= iend) {
-            v = ldg16(in + q);
-        } else {
-            // (the block's last partial chunk: one thread, byte by byte)
-            uint32_t x[4] = {0, 0, 0, 0};
-#pragma clang loop unroll(disable)
-            for (int32_t k = 0; k < 16 && q + k < iend; ++k) {
-                const uint32_t bv = ldb(in, q + k) << (8 * (k & 3));
-                x[0] |= k < 4 ? bv : 0u;
-                x[1] |= (k >> 2) == 1 ? bv : 0u;
-                x[2] |= (k >> 2) == 2 ? bv : 0u;
-                x[3] |= k >= 12 ? bv : 0u;
-            }
-            v = make_uint4(x[0], x[1], x[2], x[3]);
-        }
-        *(uint4*)(stage + 16 * i) = v;
-    }
-}
-
-// Workgroup copies for wide_exact_seq (every thread calls them; loads never
-// read at or past lim).
-LZ4E_DEV void wg_sync_stores() {
-    stores_done();
-    block_sync();
-}
-LZ4E_DEV void wg_copy(uint8_t* dst, const uint8_t* src, int32_t len, const uint8_t* lim, uint32_t tid) {
-    constexpr int32_t kU = 4, kR = 16 * kU * (int32_t)kWThreads;
-    for (int32_t t0 = 0; t0 < len; t0 += kR) {
-        uint4 v[kU];
-#pragma unroll
-        for (int32_t i = 0; i < kU; ++i) {
-            const int32_t q = t0 + 16 * ((int32_t)tid + i * (int32_t)kWThreads);
-            if (q < len) v[i] = ld16_lim(src + q, (uint32_t)(len - q < 16 ? len - q : 16), lim);
-        }
-#pragma unroll
-        for (int32_t i = 0; i < kU; ++i) {
-            const int32_t q = t0 + 16 * ((int32_t)tid + i * (int32_t)kWThreads);
-            if (q < len) st16_n(dst + q, v[i], (uint32_t)(len - q < 16 ? len - q : 16));
-        }
-    }
-}
-// dst[t] = dst[t - off] for t in [0, len), any overlap (offset 0: zeros);
-// the bytes before dst are final and visible to every thread.
-LZ4E_DEV void wg_match(uint8_t* dst, uint32_t off, int32_t len, const uint8_t* lim, uint32_t tid) {
-    if (off < 16) {
-        uint4 p = make_uint4(0, 0, 0, 0);
-        if (off != 0) p = ld16_lim(dst - off, off, lim);
-        for (int32_t t = 16 * (int32_t)tid; t < len; t += 16 * (int32_t)kWThreads) {
-            const uint4 v = off == 0 ? make_uint4(0, 0, 0, 0) : period16(p, off, (uint32_t)t % off);
-            st16_n(dst + t, v, (uint32_t)(len - t < 16 ? len - t : 16));
-        }
-        return;
-    }
-    constexpr int32_t kU = 4, kR = 16 * kU * (int32_t)kWThreads;
-    int32_t D = (int32_t)off;
-    for (int32_t t = 0; t < len;) {
-        int32_t c = len - t < D ? len - t : D;
-        c = c < kR ? c : kR;
-        uint4 v[kU];
-#pragma unroll
-        for (int32_t i = 0; i < kU; ++i) {
-            const int32_t q = 16 * ((int32_t)tid + i * (int32_t)kWThreads);
-            if (q < c) v[i] = ld16_lim(dst + t + q - D, (uint32_t)(c - q < 16 ? c - q : 16), lim);
-        }
-#pragma unroll
-        for (int32_t i = 0; i < kU; ++i) {
-            const int32_t q = 16 * ((int32_t)tid + i * (int32_t)kWThreads);
-            if (q < c) st16_n(dst + t + q, v[i], (uint32_t)(c - q < 16 ? c - q : 16));
-        }
-        wg_sync_stores();
-        t += c;
-        while (2 * D <= t) D *= 2;
-    }
-}
-
-// One sequence of the reference's loop (lz4e_decompress.c:123-446) from
-// (ip, op): the checks of group_decode / parse_batch's exact path in the
-// same order, the parse run by every thread alike (wave-uniform), the copies
-// shared.  kWMore with (ip, op) advanced, or the block's value (the output
-// size, or -(ip) - 1 at the failing read).  The output before op is final
-// and visible; so is this sequence's on return.
-LZ4E_DEV int32_t wide_exact_seq(const uint8_t* in, int32_t iend, uint8_t* out, int32_t oend, int32_t D,
-                                int32_t& ipr, int32_t& opr, uint32_t tid, uint8_t* stage, int32_t& sb) {
-    const int32_t shortiend = iend - 14 - 2, shortoend = oend - 14 - 18;  // :100-103
-    const uint8_t* ilim = in + iend;
-    const uint8_t* olim = out + oend;
-    // the input through the staged window [sb, sb + kWStage), restaged at
-    // the byte read when it leaves it (p is the same in every thread)
-    auto byte = [&](int32_t p) -> uint32_t {
-        if (p >= iend) return 0u;
-        if ((uint32_t)(p - sb) >= (uint32_t)kWStage) {
-            block_sync();
-            wide_stage(stage, in, iend, p, tid);
-            sb = p;
-            block_sync();
-        }
-        return ((const lu8*)stage)[p - sb];
-    };
-    // Length-extension run from p0: the first position q >= p0 whose byte is
-    // not 255 or that is >= plim (the reference reads such runs one byte at a
-    // time, :201-206, 319-326), 1024 bytes per step: each lane of each wave
-    // tests 4 staged bytes per round (every wave finds the same q).
-    auto ext_stop = [&](int32_t p0, int32_t plim) -> int32_t {
-        const uint32_t lane = tid % kWave;
-        for (int32_t p = p0;; p += 4 * (int32_t)kWave) {
-            if (p >= plim || p >= iend) return p;
-            if ((uint32_t)(p - sb) > (uint32_t)(kWStage - 4 * (int32_t)kWave)) {
-                block_sync();
-                wide_stage(stage, in, iend, p, tid);
-                sb = p;
-                block_sync();
-            }
-            const int32_t pa = p + 4 * (int32_t)lane;
-            const uint32_t w = ld4((const lu8*)stage + (pa - sb));
-            uint32_t m = 0;
-#pragma unroll
-            for (uint32_t t = 0; t < 4; ++t) {
-                const int32_t q = pa + (int32_t)t;
-                m |= (((w >> (8 * t)) & 0xFFu) != 0xFFu || q >= plim || q >= iend ? 1u : 0u) << t;
-            }
-            const uint64_t bm = ballot(m != 0);
-            if (bm) {
-                const uint32_t l = ctz64(bm);
-                return p + 4 * (int32_t)l + (int32_t)__builtin_ctz(lane_val(m, l));
-            }
-        }
-    };
-    int32_t ip = ipr, op = opr;
-    const uint32_t token = byte(ip);
-    ip++;
-    uint32_t length = token >> 4;  // saturates at kSat
-    int32_t offset;
-    if (length != 15 && ip < shortiend && op <= shortoend) {
-        // two-stage shortcut (:150-191)
-        if (length) wg_copy(out + op, in + ip, (int32_t)length, ilim, tid);
-        op += (int32_t)length;
-        ip += (int32_t)length;
-        offset = (int32_t)(byte(ip) | (byte(ip + 1) << 8));
-        ip += 2;
-        length = token & 15;
-        if (length != 15 && offset >= 8 && op >= offset) {
-            wg_sync_stores();
-            wg_match(out + op, (uint32_t)offset, (int32_t)length + 4, olim, tid);
-            wg_sync_stores();
-            ipr = ip;
-            opr = op + (int32_t)length + 4;
-            return kWMore;
-        }
-    } else {
-        if (length == 15) {  // :194-220
-            if (ip >= iend - 15) return -ip - 1;
-            // bytes ip .. q: 255 each, then the last; the loop goes on while
-            // the next position is below iend - 15
-            const int32_t q = ext_stop(ip, iend - 16);
-            const uint64_t sum = (uint64_t)length + 255ull * (uint64_t)(q - ip) + byte(q);
-            length = sum > kSat ? kSat : (uint32_t)sum;
-            ip = q + 1;
-        }
-        const uint32_t cpy = (uint32_t)op + length;  // :223-288
-        const uint32_t iln = (uint32_t)ip + length;
-        if (ugt(cpy, oend - 12) || ugt(iln, iend - 8)) {
-            if (iln != (uint32_t)iend || ugt(cpy, oend)) return -ip - 1;
-            wg_copy(out + op, in + ip, (int32_t)length, ilim, tid);  // final literal run
-            wg_sync_stores();
-            return (int32_t)cpy;
-        }
-        wg_copy(out + op, in + ip, (int32_t)length, ilim, tid);
-        ip += (int32_t)length;
-        op = (int32_t)cpy;
-        offset = (int32_t)(byte(ip) | (byte(ip + 1) << 8));  // :291-296
-        ip += 2;
-        length = token & 15;
-    }
-    // _copy_match (:298-336, :422-431)
-    if (op - offset + D < 0) return -ip - 1;
-    if (length == 15) {
-        // bytes ip .. q: 255 each, then the last; reading a byte at or past
-        // iend - 5 fails (ip > iend - 5 after the read)
-        const int32_t q = ext_stop(ip, iend - 5);
-        if (q + 1 > iend - 5) return -(q + 1) - 1;
-        const uint64_t sum = (uint64_t)length + 255ull * (uint64_t)(q - ip) + byte(q);
-        length = sum > kSat ? kSat : (uint32_t)sum;
-        ip = q + 1;
-    }
-    if (ugt((uint32_t)op + length + 4, oend - 5)) return -ip - 1;
-    wg_sync_stores();  // the literal run before the match's loads
-    wg_match(out + op, (uint32_t)offset, (int32_t)length + 4, olim, tid);
-    wg_sync_stores();
-    ipr = ip;
-    opr = op + (int32_t)length + 4;
-    return kWMore;
-}
-
-// A sequence's fields from the staged chunk (stage offset r of its token).
-struct WSeq {
-    int32_t lit, L, off, M, hdr;  // literal start (stage offset), lengths (M with MINMATCH), next token (stage offset)
-    int32_t lx, mx;               // extension bytes of the two lengths
-    uint32_t tok;
-    bool in_stage;                // the whole header lies in the staged bytes
-};
-// A length-extension run in the stage from q: the number of its 255 bytes
-// (n255) and its last byte's position (-1: not within the staged bytes).
-LZ4E_DEV int32_t wide_ext(const lu8* st, int32_t q, int32_t& n255) {
-    for (int32_t p = q; p < kWStage; p += 4) {
-        const uint32_t w = ld4(st + p);  // (the stage has 16 bytes of slack)
-        const uint32_t nf = ~w;          // non-0xFF bytes: a nonzero byte
-        if (nf) {
-            const int32_t k = (int32_t)__builtin_ctz(nf) >> 3;
-            n255 = p + k - q;
-            return p + k < kWStage ? p + k : -1;
-        }
-    }
-    return -1;
-}
-LZ4E_DEV WSeq wide_fields(const lu8* st, int32_t r) {
-    WSeq s;
-    s.tok = st[r];
-    int32_t q = r + 1;
-    s.L = (int32_t)(s.tok >> 4);
-    s.lx = 0;
-    s.in_stage = true;
-    s.off = 0;
-    s.M = 0;
-    s.mx = 0;
-    if (s.L == 15) {
-        int32_t n255 = 0;
-        const int32_t e = wide_ext(st, q, n255);
-        if (e < 0) {
-            s.in_stage = false;
-            s.lit = s.hdr = q;
-            return s;
-        }
-        s.L += 255 * n255 + (int32_t)st[e];
-        s.lx = n255 + 1;
-        q = e + 1;
-    }
-    s.lit = q;
-    q += s.L;
-    if (q + 2 > kWStage) {
-        s.in_stage = false;
-        s.hdr = q;
-        return s;
-    }
-    s.off = (int32_t)(st[q] | ((uint32_t)st[q + 1] << 8));
-    q += 2;
-    s.M = (int32_t)(s.tok & 15);
-    if (s.M == 15) {
-        int32_t n255 = 0;
-        const int32_t e = wide_ext(st, q, n255);
-        if (e < 0) {
-            s.in_stage = false;
-            s.hdr = q;
-            return s;
-        }
-        s.M += 255 * n255 + (int32_t)st[e];
-        s.mx = n255 + 1;
-        q = e + 1;
-    }
-    s.M += 4;
-    s.hdr = q;
-    return s;
-}
-
-// Does the reference take the sequence whose token is at ip (with fields s)
-// at output position op as a normal sequence -- no error, not the last
-// literal run (lz4e_decompress.c:123-446)?  The literal length's extension
-// loop must have stopped at its non-255 byte, not at iend - 15 (:203-205).
-LZ4E_DEV bool wide_normal(const WSeq& s, int32_t ip, int32_t op, int32_t iend, int32_t oend, int32_t D) {
-    const int32_t ip1 = ip + 1;
-    const uint32_t Lt = s.tok >> 4, Mt = s.tok & 15;
-    int32_t op2, ipm;  // output position of the match, input position after the offset
-    if (Lt != 15 && ip1 < iend - 16 && op <= oend - 32) {
-        // shortcut (:150-191)
-        op2 = op + s.L;
-        if (Mt != 15 && s.off >= 8 && op2 >= s.off) return true;
-        ipm = ip1 + s.L + 2;
-    } else {
-        if (Lt == 15) {
-            if (ip1 >= iend - 15) return false;
-            if (s.lx > 1 && ip1 + s.lx - 1 >= iend - 15) return false;  // the loop would stop early
-        }
-        const int32_t lit = ip1 + s.lx;
-        if ((int64_t)op + s.L > (int64_t)oend - 12 || (int64_t)lit + s.L > (int64_t)iend - 8) return false;
-        op2 = op + s.L;
-        ipm = lit + s.L + 2;
-    }
-    if (op2 - s.off + D < 0) return false;
-    if (Mt == 15 && ipm + s.mx > iend - 5) return false;
-    return (int64_t)op2 + s.M <= (int64_t)oend - 5;
-}
-
-// a mod b for a < 2^24, 0 < b < 2^17 (a float quotient, corrected).
-LZ4E_DEV uint32_t umod_small(uint32_t a, uint32_t b) {
-    const uint32_t q = (uint32_t)((float)a * rcp_approx((float)b));  // within 2 of a / b
-    int32_t r = (int32_t)(a - q * b);
-    r += r < 0 ? (int32_t)b : 0;
-    r += r < 0 ? (int32_t)b : 0;
-    r -= r >= (int32_t)b ? (int32_t)b : 0;
-    r -= r >= (int32_t)b ? (int32_t)b : 0;
-    return (uint32_t)r;
-}
-
-// a[c] for a small per-thread array without dynamic register indexing.
-LZ4E_DEV int32_t sel5(const int32_t* a, uint32_t c) {
-    return c == 0 ? a[0] : c == 1 ? a[1] : c == 2 ? a[2] : c == 3 ? a[3] : a[4];
-}
-
-// The last k in [0, n) with rec[k].op <= x (rec[0].op <= x).
-LZ4E_DEV uint32_t wide_find(const WideLds& S, uint32_t n, int32_t x) {
-    uint32_t lo = 0, hi = n;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if ((int32_t)S.rec[mid][0] <= x) lo = mid;
-        else hi = mid;
-    }
-    return lo;
-}
-
-// Workgroups per CU asked of the compiler (register budget; LDS allows 7).
-#ifndef LZ4E_WIDE_MINWG
-#define LZ4E_WIDE_MINWG 6
-#endif
-template <bool kStamps>
-__global__ __launch_bounds__(kWThreads, LZ4E_WIDE_MINWG) void decompress_wide_kernel(
-    const uint8_t* __restrict__ src, const uint64_t* __restrict__ src_off, const int32_t* __restrict__ src_len,
-    uint8_t* dst, const uint64_t* __restrict__ dst_off, const int32_t* __restrict__ dst_cap,
-    int32_t* __restrict__ ret, uint32_t nblocks, const int32_t* __restrict__ dict_len,
-    const uint32_t* __restrict__ order, uint32_t spb, const uint32_t* __restrict__ wmarks,
-    const int32_t* __restrict__ wexits, uint64_t* __restrict__ dbg) {
-    __shared__ __attribute__((aligned(16))) WideLds S;
-    if (blockIdx.x >= nblocks) return;
-    const uint32_t b = order ? order[blockIdx.x] : blockIdx.x;
-    const uint32_t tid = threadIdx.x, lane = tid % kWave, wave = tid / kWave;
-    const int32_t iend = src_len[b], oend = dst_cap[b];
-    const uint8_t* in = src + src_off[b];
-    uint8_t* gout = dst + dst_off[b];
-    if (special_case(in, iend, oend, ret + b, tid)) return;
-    const int32_t D = (int32_t)uni((uint32_t)dict_of(dict_len, b));  // (uniform: buffer resources)
-    const int32_t nseg = (iend + (int32_t)kWSeg - 1) / (int32_t)kWSeg;
-    const bool walked = (int64_t)iend <= (int64_t)spb * kWSeg;
-    const size_t wbase = (size_t)b * spb;
-    [[maybe_unused]] uint64_t st_chunks = 0, st_steps = 0, st_rounds = 0, st_exact = 0, st_rewalk = 0;
-    // stamped build: cycles per phase (thread 0's clock between barriers):
-    // 0 stage, 1 wave 0's token starts, 2 fields + scan + checks, 3 byte
-    // classification + external loads, 4 pointer rounds, 5 stores, 6 exact
-    [[maybe_unused]] uint64_t st_t = kStamps ? clock64() : 0, st_acc[7] = {0, 0, 0, 0, 0, 0, 0};
-    [[maybe_unused]] auto lap = [&](int k) {
-        const uint64_t now = clock64();
-        st_acc[k] += now - st_t;
-        st_t = now;
-    };
-    if (tid < 3) S.more[tid] = 0;
-    int32_t ip = 0, op = 0, result = kWMore;
-    int32_t sb = INT32_MIN / 2;  // block position of S.stage[0] (nothing staged yet)
-    for (;;) {
-        // ---------------- the next chunk's token starts ----------------
-        // (a sequence the fast path cannot take goes through wide_exact_seq
-        // below, which is also the whole decode of an unwalked block)
-        uint32_t nfast = 0, ntok = 0, bad = ~0u;
-        if (walked && ip < iend) {
-            const int32_t cb = ip & ~(int32_t)(kWSeg - 1);
-            if constexpr (kStamps) st_chunks++;
-            wide_stage(S.stage, in, iend, cb, tid);
-            sb = cb;
-            if (tid == 0) S.bad = ~0u;
-            block_sync();
-            if constexpr (kStamps) lap(0);
-            if (wave == 0) {
-                // segment lane: sc + lane; nx: the segment (relative) where
-                // its chain goes on, 64 = past the chunk or the chain's end
-                const int32_t sc = cb / (int32_t)kWSeg, seg = sc + (int32_t)lane;
-                uint32_t m = 0;
-                int32_t x = iend;
-                if (seg < nseg) {
-                    m = wmarks[wbase + (size_t)seg];
-                    x = wexits[wbase + (size_t)seg];
-                }
-                auto rb = [&](int32_t q) -> uint32_t {
-                    const uint32_t r = (uint32_t)(q - cb);
-                    if (r < (uint32_t)kWStage) return S.stage[r];
-                    return q < iend ? ldb(in, q) : 0u;
-                };
-                uint32_t P = 0, mP = 0;
-                int32_t E = ip, bit = 0;
-                bool valid = false;
-                for (;;) {
-                    const int32_t xs = x >> 5;
-                    uint32_t J = (x >= iend || x < 32 * (seg + 1) || xs - sc >= 64) ? 64u : (uint32_t)(xs - sc);
-                    // P: the lane-th segment of the path from segment 0
-                    P = 0;
-                    for (uint32_t k = 0; k < 6; ++k) {
-                        const uint32_t y = shfl(J, P & 63);
-                        if ((lane >> k) & 1) P = P < 64 ? y : 64u;
-                        const uint32_t J2 = shfl(J, J & 63);
-                        J = J < 64 ? J2 : 64u;
-                    }
-                    valid = P < 64;
-                    const uint32_t Pp = shfl(P, lane - 1);
-                    const int32_t xprev = (int32_t)shfl((uint32_t)x, Pp & 63);
-                    E = lane == 0 ? ip : xprev;
-                    mP = shfl(m, P & 63);
-                    bit = E - 32 * (sc + (int32_t)P);
-                    const bool ok = !valid || (bit >= 0 && bit < 32 && ((mP >> bit) & 1));
-                    const uint64_t fail = ballot(!ok);
-                    if (!fail) break;
-                    // walkers of segments entered off their marks did not
-                    // join the chain in time: walk each such segment from its
-                    // entry (all at once; the first one's entry is true, so
-                    // every round fixes at least one segment for good, and
-                    // the next round checks the rest against the new path)
-                    if constexpr (kStamps) st_rewalk += popc64(fail);
-                    uint32_t mm = 0;
-                    int32_t xx = 0;
-                    if (!ok) walk_segment(rb, iend, 32 * (sc + (int32_t)P), E, mm, xx);
-                    for (uint64_t f = fail; f; f &= f - 1) {
-                        const uint32_t i = ctz64(f);
-                        const uint32_t Pi = lane_val(P, i), mi = lane_val(mm, i);
-                        const int32_t xi = (int32_t)lane_val((uint32_t)xx, i);
-                        if (lane == Pi) {
-                            m = mi;
-                            x = xi;
-                        }
-                    }
-                }
-                const uint32_t tm = valid ? (mP & (~0u << (bit & 31))) : 0u;
-                const uint32_t c = popc64(tm);
-                const uint32_t incl = wave_incl_add(c);
-                uint32_t k = incl - c;
-                for (uint32_t mm = tm; mm; mm &= mm - 1) S.rec[k++][2] = (uint32_t)(32 * (sc + (int32_t)P)) + (uint32_t)__builtin_ctz(mm);
-                if (lane == kWave - 1) S.ntok = (int32_t)incl;
-            }
-            block_sync();
-            if constexpr (kStamps) lap(1);
-            ntok = (uint32_t)S.ntok;
-            // ---------------- fields, output positions, checks ----------------
-            // pass 1 the lengths, a workgroup scan, pass 2 the fields again
-            // (from LDS: cheaper than holding three sequences' fields in
-            // registers across the scan), the checks and the records
-            int32_t len[kWPer], sum = 0;
-            uint32_t pos[kWPer];
-#pragma unroll
-            for (uint32_t i = 0; i < kWPer; ++i) {
-                const uint32_t k = kWPer * tid + i;
-                len[i] = 0;
-                pos[i] = 0;
-                if (k < ntok) {
-                    pos[i] = S.rec[k][2];
-                    const WSeq q = wide_fields((const lu8*)S.stage, (int32_t)pos[i] - cb);
-                    len[i] = q.in_stage ? q.L + q.M : 0;
-                }
-                sum += len[i];
-            }
-            const int32_t wincl = (int32_t)wave_incl_add((uint32_t)sum);
-            if (lane == kWave - 1) S.wsum[wave] = wincl;
-            block_sync();
-            int32_t o = op + wincl - sum;
-            for (uint32_t w = 0; w < wave; ++w) o += S.wsum[w];
-            uint32_t badk = ~0u;
-            int32_t hdr[kWPer];
-#pragma unroll
-            for (uint32_t i = 0; i < kWPer; ++i) {
-                const uint32_t k = kWPer * tid + i;
-                hdr[i] = 0;
-                if (k < ntok) {
-                    const WSeq q = wide_fields((const lu8*)S.stage, (int32_t)pos[i] - cb);
-                    const bool normal = q.in_stage && wide_normal(q, (int32_t)pos[i], o, iend, oend, D);
-                    if (!normal && badk == ~0u) badk = (k << 1) | (q.in_stage ? 0u : 1u);
-                    S.rec[k][0] = (uint32_t)o;
-                    S.rec[k][1] = (uint32_t)q.lit | ((uint32_t)q.L << 16);
-                    S.rec[k][2] = (uint32_t)q.off;
-                    hdr[i] = cb + q.hdr;
-                    o += len[i];
-                }
-            }
-            if (badk != ~0u) atomicMin(&S.bad, badk);
-            block_sync();
-            bad = S.bad;
-            nfast = bad == ~0u ? ntok : (bad >> 1);
-            if (nfast > 0 && kWPer * tid <= nfast - 1 && nfast - 1 < kWPer * tid + kWPer) {
-                const uint32_t i = nfast - 1 - kWPer * tid;
-                S.opE = (int32_t)S.rec[nfast - 1][0] + (i == 0 ? len[0] : i == 1 ? len[1] : len[2]);
-                S.next_ip = i == 0 ? hdr[0] : i == 1 ? hdr[1] : hdr[2];
-            }
-            block_sync();
-            if constexpr (kStamps) lap(2);
-        }
-        // ---------------- assemble the fast sequences' output ----------------
-        if (nfast > 0) {
-            const int32_t opE = S.opE;
-            for (int32_t O = op; O < opE; O += kWStep) {
-                if constexpr (kStamps) st_steps++;
-                // thread tid owns the 16 bytes at O + kWGroup g + 16 tid of
-                // each group g
-                bool anyp[kWGroups];
-#pragma unroll 1
-                for (uint32_t g = 0; g < kWGroups; ++g) {
-                    const int32_t xo = (int32_t)(kWGroup * g + 16 * tid);  // step index of my first byte
-                    const int32_t x0 = O + xo;
-                    const int32_t nb = opE - x0 < 16 ? opE - x0 : 16;  // bytes of mine (<= 0: none)
-                    anyp[g] = false;
-                    if (nb <= 0) continue;
-                    // the (at most 5) sequences my 16 bytes belong to: output
-                    // start and end, literal start | length << 16, offset
-                    const uint32_t k0 = wide_find(S, nfast, x0);
-                    int32_t sop[5], send[5], sll[5], soff[5];
-#pragma unroll
-                    for (uint32_t i = 0; i < 5; ++i) {
-                        const uint32_t k = k0 + i < nfast ? k0 + i : nfast - 1;
-                        sop[i] = (int32_t)S.rec[k][0];
-                        sll[i] = (int32_t)S.rec[k][1];
-                        soff[i] = (int32_t)S.rec[k][2];
-                        send[i] = k0 + i + 1 < nfast ? (int32_t)S.rec[k0 + i + 1][0] : opE;
-                    }
-                    // v[j]: kVLit (the literal byte lb[j]), kVFin (a zero:
-                    // offset 0), kVExt | (source + D) (final in HBM: hb[j]),
-                    // or the step index of the source (a pointer).  Branch-
-                    // free: every LDS and HBM read of the 16 bytes is issued
-                    // unconditionally (a dummy index where unused), so they
-                    // are all in flight together.
-                    constexpr uint32_t kVFin = 1u << 31, kVExt = 1u << 30, kVLit = 1u << 29;
-                    uint32_t c = 0, v[16], lb[16];
-#pragma unroll
-                    for (int32_t j = 0; j < 16; ++j) {
-                        const int32_t x = x0 + j;
-                        c += (c < 4 && x >= sel5(send, c)) ? 1u : 0u;
-                        const int32_t so = sel5(sop, c), ll = sel5(sll, c), of = sel5(soff, c);
-                        const int32_t sl = (int32_t)((uint32_t)ll >> 16);
-                        const int32_t r = x - so;
-                        const bool lit = r < sl;
-                        lb[j] = S.stage[lit ? (ll & 0xFFFF) + r : 0];
-                        int32_t mm = r - sl;
-                        if (mm >= of && of != 0) mm = (int32_t)umod_small((uint32_t)mm, (uint32_t)of);
-                        const int32_t sx = so + sl - of + mm;
-                        v[j] = j >= nb ? kVFin
-                               : lit   ? kVLit
-                               : (of == 0 ? kVFin : (sx < O ? kVExt | (uint32_t)(sx + D) : (uint32_t)(sx - O)));
-                    }
-                    // (32-bit offsets into one buffer resource: one VGPR per
-                    // address)
-                    const ByteBuf gb = buf_make(gout - D, (uint32_t)(D + oend));
-                    uint32_t hb[16];
-#pragma unroll
-                    for (int32_t j = 0; j < 16; ++j) hb[j] = buf_ld8(gb, (v[j] & kVExt) ? v[j] & (kVExt - 1) : 0u);
-                    uint32_t w[8];
-                    bool ap = false;
-#pragma unroll
-                    for (int32_t j = 0; j < 16; j += 2) {
-                        uint32_t e2[2];
-#pragma unroll
-                        for (int32_t h = 0; h < 2; ++h) {
-                            const uint32_t vj = v[j + h];
-                            e2[h] = (vj & kVLit)   ? (kWFinal | lb[j + h])
-                                    : (vj & kVExt) ? (kWFinal | hb[j + h])
-                                    : (vj & kVFin) ? kWFinal
-                                                   : vj;
-                            ap |= !(e2[h] & kWFinal);
-                        }
-                        w[j >> 1] = e2[0] | (e2[1] << 16);
-                    }
-                    anyp[g] = ap;
-                    *(uint4*)&S.ent[xo] = make_uint4(w[0], w[1], w[2], w[3]);
-                    *(uint4*)&S.ent[xo + 8] = make_uint4(w[4], w[5], w[6], w[7]);
-                }
-                // pointer jumping until every byte of the step is final
-                if (anyp[0] || anyp[1]) S.more[0] = 1;
-                block_sync();
-                if constexpr (kStamps) lap(3);
-                for (uint32_t rd = 0; S.more[rd % 3]; ++rd) {
-                    if constexpr (kStamps) st_rounds++;
-                    if (tid == 0) S.more[(rd + 2) % 3] = 0;
-                    bool again = false;
-#pragma unroll 1
-                    for (uint32_t g = 0; g < kWGroups; ++g) {
-                        if (!anyp[g]) continue;
-                        const int32_t xo = (int32_t)(kWGroup * g + 16 * tid);
-                        const uint4 a0 = *(const uint4*)&S.ent[xo], a1 = *(const uint4*)&S.ent[xo + 8];
-                        uint32_t w[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                        bool ag = false;
-#pragma unroll
-                        for (int32_t j = 0; j < 16; ++j) {
-                            const uint32_t sh = 16 * (j & 1);
-                            uint32_t e = (w[j >> 1] >> sh) & 0xFFFFu;
-                            if (!(e & kWFinal)) {
-                                e = S.ent[e];
-                                ag |= !(e & kWFinal);
-                                w[j >> 1] = (w[j >> 1] & ~(0xFFFFu << sh)) | (e << sh);
-                            }
-                        }
-                        *(uint4*)&S.ent[xo] = make_uint4(w[0], w[1], w[2], w[3]);
-                        *(uint4*)&S.ent[xo + 8] = make_uint4(w[4], w[5], w[6], w[7]);
-                        anyp[g] = ag;
-                        again |= ag;
-                    }
-                    if (again) S.more[(rd + 1) % 3] = 1;
-                    block_sync();
-                    if constexpr (kStamps) lap(4);
-                }
-                if (tid == 0) S.more[0] = S.more[1] = S.more[2] = 0;  // (the next step starts at round 0)
-                // store pass
-#pragma unroll 1
-                for (uint32_t g = 0; g < kWGroups; ++g) {
-                    const int32_t xo = (int32_t)(kWGroup * g + 16 * tid);
-                    const int32_t x0 = O + xo;
-                    const int32_t nb = opE - x0 < 16 ? opE - x0 : 16;
-                    if (nb <= 0) continue;
-                    const uint4 a0 = *(const uint4*)&S.ent[xo], a1 = *(const uint4*)&S.ent[xo + 8];
-                    const uint32_t w[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-                    uint32_t o4[4];
-#pragma unroll
-                    for (int32_t q = 0; q < 4; ++q)
-                        o4[q] = (w[2 * q] & 0xFFu) | ((w[2 * q] >> 8) & 0xFF00u) | ((w[2 * q + 1] & 0xFFu) << 16) |
-                                ((w[2 * q + 1] << 8) & 0xFF000000u);
-                    const uint4 vv = make_uint4(o4[0], o4[1], o4[2], o4[3]);
-                    if (nb == 16) stg16(gout + x0, vv);
-                    else gst_tail(gout + x0, vv, (uint32_t)nb);
-                }
-                wg_sync_stores();
-                if constexpr (kStamps) lap(5);
-            }
-            op = opE;
-            ip = S.next_ip;
-            if (nfast < ntok && (bad & 1u)) continue;  // a header past the staged bytes: the next chunk
-            if (nfast == ntok) continue;
-        }
-        // ---------------- one sequence the fast path did not take ----------------
-        if constexpr (kStamps) st_exact++;
-        result = wide_exact_seq(in, iend, gout, oend, D, ip, op, tid, S.stage, sb);
-        if constexpr (kStamps) lap(6);
-        if (result != kWMore) break;
-    }
-    if (tid == 0) ret[b] = result;
-    if constexpr (kStamps) {
-        if (tid == 0 && dbg) {
-            uint64_t* d = dbg + 16 * (size_t)b;  // (16 words per block)
-            d[0] = st_chunks;
-            d[1] = st_steps;
-            d[2] = st_rounds;
-            d[3] = st_exact;
-            d[4] = st_rewalk;
-            for (int k = 0; k < 7; ++k) d[8 + k] = st_acc[k];
-        }
-    }
-}
-
 // Blocks whose capacity lies in [kPipeMinCap, kPipeMaxCap) take the
 // pipelined decoder.  Small blocks parse in a few batches, and one wave each
 // keeps more of them resident.  Large blocks (256 KiB: ~560 batches each)
@@ -3068,7 +2256,6 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
                : env[0] == 'p' ? kDecPipe
                : env[0] == 's' ? kDecSmall
                : env[0] == 'g' ? kDecGroup
-               : env[0] == 'x' ? kDecWide
                                : kDecAuto;
     if (mode == kDecAuto)
         mode = (a.max_cap == 0 || (a.max_cap >= kPipeMinCap && a.max_cap < kPipeMaxCap))
@@ -3079,40 +2266,6 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
                                  ? kDecPipe
                                  : (a.max_cap <= (uint32_t)kSmallOut && a.nblocks <= kSmallMaxBlocks ? kDecSmall
                                                                                                      : kDecWave)));
-    if (mode == kDecWide && a.max_cap == 0) mode = kDecPipe;  // (the walkers' scratch is sized by max_cap)
-    if (mode == kDecWide) {
-        // walker marks + exits for compressed blocks of up to
-        // LZ4E_COMPRESSBOUND(max_cap) bytes (larger ones: wide_exact_seq
-        // alone), then the launch order, in one stream-ordered allocation
-        const uint64_t bound = (uint64_t)a.max_cap + a.max_cap / 255 + 16;
-        uint32_t spb = (uint32_t)((bound + kWSeg - 1) / kWSeg);
-        const uint32_t wpb = (spb + kWThreads - 1) / kWThreads;
-        const size_t nseg = (size_t)a.nblocks * spb;
-        uint32_t* scratch = nullptr;
-        if (hipMallocAsync((void**)&scratch, 4 * (2 * nseg + a.nblocks), stream) != hipSuccess) {
-            (void)hipGetLastError();
-            scratch = nullptr;
-            spb = 0;  // every block by wide_exact_seq: slow, exact
-        }
-        uint32_t* marks = scratch;
-        int32_t* exits = scratch ? (int32_t*)(scratch + nseg) : nullptr;
-        uint32_t* order = nullptr;
-        const int om = launch_order_mode(false);
-        if (scratch && (om == kOrderAlways || (om == kOrderAuto && a.nblocks > kOrderMin))) {
-            order = scratch + 2 * nseg;
-            hipLaunchKernelGGL((order_kernel<DecodeWeight>), dim3(1), dim3(kOrderThreads), 0, stream,
-                               DecodeWeight{a.src_len, a.dst_cap}, a.nblocks, order);
-        }
-        if (scratch)
-            hipLaunchKernelGGL(decompress_walk_kernel, dim3(a.nblocks * wpb), dim3(kWThreads), 0, stream, a.src,
-                               a.src_off, a.src_len, a.nblocks, wpb, spb, marks, exits);
-        hipLaunchKernelGGL((decompress_wide_kernel<kStamps>), dim3(a.nblocks), dim3(kWThreads), 0, stream, a.src,
-                           a.src_off, a.src_len, a.dst, a.dst_off, a.dst_cap, a.ret, a.nblocks, a.dict_len,
-                           (const uint32_t*)order, spb, (const uint32_t*)marks, (const int32_t*)exits, dbg);
-        const hipError_t err = hipGetLastError();
-        if (scratch) (void)hipFreeAsync(scratch, stream);
-        return err;
-    }
     if (mode == kDecPipe) {
         const int om = launch_order_mode(false);
         uint32_t* order = nullptr;

@@ -41,7 +41,7 @@ struct DecompressBatch {
     // Upper bound of dst_cap[] (0: unknown); with the batch size it selects
     // the decoder (launch_impl in lz4e_decompress.hip lists the order).
     uint32_t max_cap;
-    uint32_t mode = 0;  // kDecAuto, or force kDecWave / kDecPipe / kDecSmall / kDecGroup / kDecWide (tests, A/B)
+    uint32_t mode = 0;  // kDecAuto, or force kDecWave / kDecPipe / kDecSmall / kDecGroup (tests, A/B)
     // Dictionary mode (nullable): block i decodes with the dict_len[i] bytes
     // right before dst + dst_off[i] as its dictionary (extDict semantics of
     // lz4e_decompress.c:299-302, 339-378; <= 64 KiB of it is ever read).
@@ -50,7 +50,7 @@ struct DecompressBatch {
 
 // (3 was the streaming decoder, removed in round 4; 4 and 5 the chunked and
 // relay decoders, removed in round 5: none was ever picked by auto mode)
-enum : uint32_t { kDecAuto = 0, kDecWave = 1, kDecPipe = 2, kDecSmall = 6, kDecGroup = 7, kDecWide = 8 };
+enum : uint32_t { kDecAuto = 0, kDecWave = 1, kDecPipe = 2, kDecSmall = 6, kDecGroup = 7 };
 
 // Launch order policy (lz4e_order.h): 0 block order, 1 heavy first when the
 // batch is large enough (default), 2 heavy first always.  From

@@ -872,7 +872,7 @@ int lz4e_debug_clock_probe(void* stream, uint64_t* out, uint32_t iters) {
 }
 
 // Diagnostic (not part of include/lz4e.h): the decompress kernels with a
-// forced decoder (mode 0 auto, 1 one wave per block, 2 pipelined, 6 LDS form, 7 group, 8 wide)
+// forced decoder (mode 0 auto, 1 one wave per block, 2 pipelined, 6 LDS form, 7 lane)
 // and, when dbg is not null, the stamped build's per-block cycle counters
 // (one-wave decoder: 8 x u64 per block; pipelined and streaming: 20 x u64,
 // tools/decab.py, tools/streamab.py; dbg zeroed by the caller).
@@ -881,7 +881,7 @@ int lz4e_debug_decompress_stamped(const uint8_t* src, const uint64_t* src_off, c
                                   int32_t* ret, uint32_t nblocks, void* stream, uint64_t* dbg,
                                   uint32_t max_cap, uint32_t mode) {
     if (mode != lz4e::kDecAuto && mode != lz4e::kDecWave && mode != lz4e::kDecPipe && mode != lz4e::kDecSmall &&
-        mode != lz4e::kDecGroup && mode != lz4e::kDecWide)
+        mode != lz4e::kDecGroup)
         return -1;
     lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap, mode};
     const hipStream_t s = static_cast<hipStream_t>(stream);

@@ -150,12 +150,6 @@ LZ4E_DEV int32_t wave_excl_max(int32_t v) { return wave_excl_minmax<true>(v); }
 LZ4E_DEV uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
     return __builtin_amdgcn_alignbyte(hi, lo, r);
 }
-// v_rcp_f32: 1 / x to 1 ulp.
-#ifndef LZ4E_EMU
-LZ4E_DEV float rcp_approx(float x) { return __builtin_amdgcn_rcpf(x); }
-#else
-inline float rcp_approx(float x) { return 1.0f / x; }
-#endif
 // s_memtime: shader clock (diagnostic builds only).
 LZ4E_DEV uint64_t clock64() { return __builtin_amdgcn_s_memtime(); }
 #ifndef LZ4E_EMU

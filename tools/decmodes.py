@@ -1,6 +1,5 @@
 """Diagnostic: decoder kernels side by side -- the one-wave decoder (1), the
-pipelined 4-wave decoder (2), the LDS form (6), the group decoder (7) and the
-wide decoder (8) on the same frames
+pipelined 4-wave decoder (2) and the chunked decoder (4) on the same frames
 (compressed on the GPU), kernel time by HIP events (median of the timed
 launches after one warm-up; outputs checked equal to the input and the
 return values to the block sizes).
@@ -22,7 +21,7 @@ L = lz4e_amd.lib()
 P = ctypes.c_void_p
 L.lz4e_debug_decompress_stamped.argtypes = [P] * 7 + [ctypes.c_uint32, P, P, ctypes.c_uint32,
                                                        ctypes.c_uint32]
-NAMES = {1: "one-wave", 2: "pipelined", 6: "lds-small", 7: "group", 8: "wide"}
+NAMES = {1: "one-wave", 2: "pipelined", 6: "lds-small", 7: "group"}
 
 
 def class_blocks(kind, n, bs):

@@ -17,15 +17,12 @@
 
 // Block i decodes src_len[i] bytes at src + src_off[i] into dst + dst_off[i]
 // (capacity dst_cap[i]), dictionary: the dict_len[i] bytes before it
-// (dict_len nullable).  mode: 1 one-wave decoder, 2 pipelined decoder, 6 LDS form,
-// 7 group decoder, 8 wide decoder.
+// (dict_len nullable).  mode: 1 one-wave decoder, 2 pipelined decoder.
 extern "C" int emu_decompress_batch_mode(const uint8_t* src, const uint64_t* src_off,
                                          const int32_t* src_len, uint8_t* dst, const uint64_t* dst_off,
                                          const int32_t* dst_cap, int32_t* ret, uint32_t nblocks,
                                          const int32_t* dict_len, uint32_t mode) {
-    uint32_t max_cap = 0;  // (the wide decoder sizes its walker scratch by it)
-    for (uint32_t i = 0; i < nblocks; ++i) max_cap = dst_cap[i] > (int32_t)max_cap ? (uint32_t)dst_cap[i] : max_cap;
-    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap,
+    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, 0,
                             mode, dict_len};
     return lz4e::launch_decompress(a, nullptr) == hipSuccess ? 0 : -1;
 }
