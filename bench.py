@@ -407,7 +407,7 @@ def block_floor(b: "Batch", top: int = 4, cands: int = 32, reps: int = 5) -> dic
     L = lz4e_amd.lib()
     P = ctypes.c_void_p
     L.lz4e_debug_compress_stamped.argtypes = [P] * 8 + [ctypes.c_uint32, ctypes.c_uint32, P, P]
-    dbg = torch.zeros(b.nblk * 8, dtype=torch.int64, device=b.dev)
+    dbg = torch.zeros(b.nblk * 16, dtype=torch.int64, device=b.dev)
     rc = L.lz4e_debug_compress_stamped(b.d_src.data_ptr(), b.d_off.data_ptr(), b.d_len.data_ptr(),
                                        b.d_tt.data_ptr(), b.d_dst.data_ptr(), b.d_doff.data_ptr(),
                                        b.d_cap.data_ptr(), b.d_ret.data_ptr(), b.nblk, b.bs,
@@ -415,8 +415,8 @@ def block_floor(b: "Batch", top: int = 4, cands: int = 32, reps: int = 5) -> dic
     torch.cuda.synchronize(b.dev)
     if rc != 0:
         raise SystemExit("bench: stamped compress failed: " + lz4e_amd.last_error())
-    cyc = dbg.view(b.nblk, 8)[:, :6].sum(1).cpu().numpy()
-    one = torch.zeros(8, dtype=torch.int64, device=b.dev)
+    cyc = dbg.view(b.nblk, 16)[:, :6].sum(1).cpu().numpy()
+    one = torch.zeros(16, dtype=torch.int64, device=b.dev)
     lone = []
     for i in np.argsort(cyc)[::-1][:cands]:
         i = int(i)

@@ -124,10 +124,12 @@ struct LdsImage {
 
 // Phase cycle counters of the diagnostic build (launch_compress_stamped).
 struct Stamps {
-    uint64_t t, acc[6];
+    uint64_t t, acc[6], t0, r0;
     uint32_t cnt[4];
     LZ4E_DEV void start() {
         t = clock64();
+        t0 = t;
+        r0 = realtime64();
         for (int i = 0; i < 6; ++i) acc[i] = 0;
         for (int i = 0; i < 4; ++i) cnt[i] = 0;
     }
@@ -1027,6 +1029,9 @@ last_literals: {
                 for (int i = 0; i < 6; ++i) dbg[i] = st.acc[i];
                 dbg[6] = ((uint64_t)st.cnt[1] << 32) | st.cnt[0];
                 dbg[7] = ((uint64_t)st.cnt[3] << 32) | st.cnt[2];
+                // the parse's shader cycles and 100 MHz ticks (its clock)
+                dbg[8] = clock64() - st.t0;
+                dbg[9] = realtime64() - st.r0;
             }
         }
         return res;
@@ -1119,7 +1124,7 @@ __global__ __launch_bounds__(64) void compress_kernel(const uint8_t* __restrict_
     const uint32_t cap = dst_cap[b];
     gu8* out = (gu8*)(dst + dst_off[b]);
     const uint8_t* in = src + src_off[b];
-    uint64_t* dbg_slot = dbg ? dbg + 8 * (size_t)b : nullptr;
+    uint64_t* dbg_slot = dbg ? dbg + kCompressStampWords * (size_t)b : nullptr;
 
     // Dictionary mode: the dict_len[b] (<= 64 KiB) bytes before the block
     // are its dictionary; under 8 bytes it is ignored (LZ4_loadDict:

@@ -1032,7 +1032,7 @@ constexpr uint32_t kLaneFirstLit = LZ4E_LANE_FIRST_LIT;  // (fio-style: 256)
 // same scalar parse (their input window loads are one address per group).
 // s: the lane's index in its group; dst and src are the group's.
 
-// LZ4E_GROUP: lanes per block (2 .. 16; experiments).
+// LZ4E_GROUP: lanes per block (2 .. 16, a power of two; experiments).
 #ifndef LZ4E_GROUP
 #define LZ4E_GROUP 8
 #endif
@@ -1042,7 +1042,8 @@ constexpr uint32_t kGroup = LZ4E_GROUP;
 // share one in-order counter, so a load after a store waits for the store).
 constexpr int32_t kRound = 256;
 constexpr uint32_t kPer = kRound / (16 * kGroup);
-static_assert(kPer >= 1 && kPer * 16 * kGroup == kRound, "lanes per block: 1 .. 16, a power of two");
+static_assert(kGroup >= 2 && kGroup <= 16 && (kGroup & (kGroup - 1)) == 0 && kPer * 16 * kGroup == kRound,
+              "lanes per block: 2 .. 16, a power of two (the emulator's group barriers exist for 2 .. 32)");
 
 // Literal run: dst[t] = src[t] for t in [0, len), src a different buffer;
 // loads never read at or past lim.
@@ -1370,6 +1371,11 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
                            lu32* ring, lu16* jump, int32_t dict, lu8* sinkb, lu8* obuf = nullptr,
                            lu8* lin = nullptr, int32_t ip0 = 0, int32_t op0 = 0) {
     WaveStamps st;
+    [[maybe_unused]] uint64_t t_start = 0, r_start = 0;
+    if constexpr (kStamps) {
+        t_start = clock64();
+        r_start = realtime64();
+    }
     auto lap = [&](int ph) {
         if constexpr (kStamps) {
             const uint64_t now = clock64();
@@ -1499,6 +1505,8 @@ LZ4E_DEV void decode_block(const uint8_t* in, int32_t srcSize, uint8_t* gout, in
             dbg[3] = st.batches;
             dbg[4] = st.rounds;
             dbg[5] = st.acc[3];
+            dbg[6] = clock64() - t_start;     // the block's shader cycles
+            dbg[7] = realtime64() - r_start;  // and its 100 MHz ticks (its clock)
         }
     }
 }
@@ -1725,20 +1733,34 @@ struct PipeLds {
     int32_t abort;                             // a wait timed out (watchdog): every wave leaves
     int32_t beat;                              // heartbeat of a long in-HBM copy (watchdog)
     int32_t result;                            // the parse's return value (decided by wave 0)
+    uint32_t spin_max;                         // the watchdog's limit for this block (see below)
 };
 
-// Watchdog of the waits: ~2^23 sleeps (~1 s) in a row during which the
-// counter a wait watches does not move means a broken invariant; the block
+// Watchdog of the waits: a wait that sees the counters it watches stand
+// still for S.spin_max sleeps in a row means a broken invariant; the block
 // then fails (ret = kPipeAbort = LZ4E_DECODE_ABORTED, include/lz4e.h: the
 // host entry points report it through lz4e_last_error) instead of hanging.
-// Progress resets the count, so a wait behind one long HBM copy (a huge run
-// near LZ4E_MAX_INPUT_SIZE, copied 4 KiB per round trip) never fires it
-// while the copier ahead of it keeps moving its counter.  LZ4E_SPIN_MAX
-// overrides the limit (the emulator's watchdog test builds a small one).
+// The bound, from the frame's own worst case ("Watchdog"):
+// between two moves of a watched counter a valid frame's decode does one
+// of (a) a batch's parse and copies (<= 64 sequences, <= 1 KiB of output:
+// tens of k cycles), (b) a scalar sequence's copy in HBM, which bumps
+// `beat` every round trip, or (c) the parser's vector scan of one length-
+// extension run, 256 bytes per ~1-2 k-cycle step and no counter moved:
+// at most srcSize / 256 steps.  A sleep is >= 128 cycles (s_sleep 2), so
+// spin_max = kSpinMax (2^23 sleeps, ~0.6 s at 2.4 GHz, for (a) and
+// anything the hardware adds) + srcSize >> kSpinBytesShift sleeps (64 per
+// 256 bytes: 4-8x the scan's worst case) can only fire on a broken
+// invariant.  Progress resets the count.  LZ4E_SPIN_MAX / _BYTES_SHIFT
+// override the terms (the emulator's watchdog test builds a limit of one
+// sleep and no per-byte term).
 #ifndef LZ4E_SPIN_MAX
 #define LZ4E_SPIN_MAX (1u << 23)
 #endif
+#ifndef LZ4E_SPIN_BYTES_SHIFT
+#define LZ4E_SPIN_BYTES_SHIFT 2
+#endif
 constexpr uint32_t kSpinMax = LZ4E_SPIN_MAX;
+constexpr uint32_t kSpinBytesShift = LZ4E_SPIN_BYTES_SHIFT;
 constexpr int32_t kPipeAbort = kDecodeAborted;  // lz4e_results.h
 
 LZ4E_DEV int32_t lds_acquire(int32_t* p) {
@@ -1769,10 +1791,11 @@ LZ4E_DEV int32_t wave_min_i32(int32_t v) {
 // for batch j-1 (resolved), for the in-order store flag, batches; copier
 // phases: loads + span setup, internal rounds, cross gather, store pass,
 // store completion; internal rounds, batches with internal pointers; copier
-// pointer entries; parser phases: window, table composition, follow, fields.
+// pointer entries; parser phases: window, table composition, follow, fields;
+// the block's shader cycles and 100 MHz ticks (wave 0, start to end).
 enum { kStParse, kStPWait, kStWork, kStRec, kStFar, kStPrev, kStStore, kStBatches, kStLoads,
        kStRounds, kStGather, kStSpass, kStVm, kStNRounds, kStNInt, kStPtrs,
-       kStPWin, kStPComp, kStPFollow, kStPFields, kStSlots };
+       kStPWin, kStPComp, kStPFollow, kStPFields, kStT, kStR, kStSlots };
 // The accumulators live in LDS (a row per wave), so that the stamped build
 // has the register allocation of the real one.
 struct PipeStamps {
@@ -1801,7 +1824,7 @@ LZ4E_DEV bool wait_for(SL& S, F ready, W watch) {
             last = now;
             k = 0;
         }
-        if (k >= kSpinMax || lds_acquire(&S.abort)) {
+        if (k >= S.spin_max || lds_acquire(&S.abort)) {
             lds_release(&S.abort, 1);
             return false;
         }
@@ -2055,14 +2078,18 @@ __global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_MINWG) void decompres
         S.abort = 0;
         S.beat = 0;
         S.result = kPipeAbort;
+        S.spin_max = kSpinMax + (kSpinBytesShift < 31 ? (uint32_t)srcSize >> kSpinBytesShift : 0u);
     }
     __syncthreads();
     PipeStamps st;
     __shared__ uint64_t st_rows[kStamps ? kPipeWaves * kStSlots : 1];
+    [[maybe_unused]] uint64_t t_start = 0, r_start = 0;
     if (kStamps) {
         st.acc = st_rows + wave * kStSlots;
         if (lane < kStSlots) st.acc[lane] = 0;
         st.t = clock64();
+        t_start = st.t;
+        r_start = realtime64();
     }
 
     if (wave == 0) {
@@ -2181,6 +2208,10 @@ __global__ __launch_bounds__(kPipeWaves * kWave, LZ4E_PIPE_MINWG) void decompres
                                ? kPipeAbort
                                : S.result;
     if constexpr (kStamps) {
+        if (lane == 0 && wave == 0) {
+            st.acc[kStT] = clock64() - t_start;     // the block's shader cycles
+            st.acc[kStR] = realtime64() - r_start;  // and its 100 MHz ticks (its clock)
+        }
         if (lane == 0 && dbg) {
             uint64_t* d = dbg + kStSlots * (size_t)b;
             for (int k = 0; k < kStSlots; ++k)
@@ -2284,12 +2315,12 @@ hipError_t launch_impl(const DecompressBatch& a, hipStream_t stream, uint64_t* d
         if (order) (void)hipFreeAsync(order, stream);
         return err;
     }
-    if (mode == kDecGroup) {
-        // hand-over list (count + 3 words per block); without it every lane
-        // decodes its block to the end
+    if (mode == kDecGroup || mode == kDecGroupNoBail) {
+        // hand-over list (count + 3 words per block); without it (or in the
+        // no-hand-over test mode) every group decodes its block to the end
         uint32_t* ho = nullptr;
-        if (hipMallocAsync((void**)&ho, 4 + 12 * (size_t)a.nblocks, stream) != hipSuccess ||
-            hipMemsetAsync(ho, 0, 4, stream) != hipSuccess) {
+        if (mode == kDecGroup && (hipMallocAsync((void**)&ho, 4 + 12 * (size_t)a.nblocks, stream) != hipSuccess ||
+                                  hipMemsetAsync(ho, 0, 4, stream) != hipSuccess)) {
             (void)hipGetLastError();
             if (ho) (void)hipFreeAsync(ho, stream);
             ho = nullptr;

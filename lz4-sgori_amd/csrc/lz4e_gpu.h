@@ -41,7 +41,7 @@ struct DecompressBatch {
     // Upper bound of dst_cap[] (0: unknown); with the batch size it selects
     // the decoder (launch_impl in lz4e_decompress.hip lists the order).
     uint32_t max_cap;
-    uint32_t mode = 0;  // kDecAuto, or force kDecWave / kDecPipe / kDecSmall / kDecGroup (tests, A/B)
+    uint32_t mode = 0;  // kDecAuto, or force kDecWave / kDecPipe / kDecSmall / kDecGroup / kDecGroupNoBail (tests, A/B)
     // Dictionary mode (nullable): block i decodes with the dict_len[i] bytes
     // right before dst + dst_off[i] as its dictionary (extDict semantics of
     // lz4e_decompress.c:299-302, 339-378; <= 64 KiB of it is ever read).
@@ -50,7 +50,10 @@ struct DecompressBatch {
 
 // (3 was the streaming decoder, removed in round 4; 4 and 5 the chunked and
 // relay decoders, removed in round 5: none was ever picked by auto mode)
-enum : uint32_t { kDecAuto = 0, kDecWave = 1, kDecPipe = 2, kDecSmall = 6, kDecGroup = 7 };
+// kDecGroupNoBail: the group decoder with its hand-over to the one-wave
+// decoder disabled -- every block decoded to its end by its group (tests and
+// A/B only; auto mode never picks it).
+enum : uint32_t { kDecAuto = 0, kDecWave = 1, kDecPipe = 2, kDecSmall = 6, kDecGroup = 7, kDecGroupNoBail = 9 };
 
 // Launch order policy (lz4e_order.h): 0 block order, 1 heavy first when the
 // batch is large enough (default), 2 heavy first always.  From
@@ -61,7 +64,10 @@ int launch_order_mode(bool compress);
 
 uint32_t compress_lds_bytes(uint32_t max_len, bool lds_input);
 hipError_t launch_compress(const CompressBatch& a, hipStream_t stream);
-// Diagnostic build: per-block phase cycle counters (8 x u64 per block) into dbg.
+// Diagnostic build: per-block phase cycle counters into dbg, kCompressStampWords
+// x u64 per block: 6 phase cycle sums, 2 packed counts, the parse's shader
+// cycles and its 100 MHz (s_memrealtime) ticks.
+constexpr uint32_t kCompressStampWords = 16;
 hipError_t launch_compress_stamped(const CompressBatch& a, hipStream_t stream, uint64_t* dbg);
 hipError_t launch_decompress(const DecompressBatch& a, hipStream_t stream);
 hipError_t launch_decompress_stamped(const DecompressBatch& a, hipStream_t stream, uint64_t* dbg);

@@ -872,16 +872,19 @@ int lz4e_debug_clock_probe(void* stream, uint64_t* out, uint32_t iters) {
 }
 
 // Diagnostic (not part of include/lz4e.h): the decompress kernels with a
-// forced decoder (mode 0 auto, 1 one wave per block, 2 pipelined, 6 LDS form, 7 lane)
-// and, when dbg is not null, the stamped build's per-block cycle counters
-// (one-wave decoder: 8 x u64 per block; pipelined and streaming: 20 x u64,
-// tools/decab.py, tools/streamab.py; dbg zeroed by the caller).
+// forced decoder (mode 0 auto, 1 one wave per block, 2 pipelined, 6 LDS form,
+// 7 group, 9 group without the hand-over) and, when dbg is not null, the
+// stamped build's per-block cycle counters (one-wave decoder and the blocks
+// the group decoder hands over: 8 x u64 per block; pipelined: 22 x u64,
+// tools/dstamps.py, tools/single_call_clock.py; dbg zeroed by the caller).
+// The group decoder keeps no stamps of its own: in mode 7 a block it decodes
+// to the end leaves its row zero, and mode 9 leaves every row zero.
 int lz4e_debug_decompress_stamped(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
                                   uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap,
                                   int32_t* ret, uint32_t nblocks, void* stream, uint64_t* dbg,
                                   uint32_t max_cap, uint32_t mode) {
     if (mode != lz4e::kDecAuto && mode != lz4e::kDecWave && mode != lz4e::kDecPipe && mode != lz4e::kDecSmall &&
-        mode != lz4e::kDecGroup)
+        mode != lz4e::kDecGroup && mode != lz4e::kDecGroupNoBail)
         return -1;
     lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap, mode};
     const hipStream_t s = static_cast<hipStream_t>(stream);
@@ -919,6 +922,22 @@ int lz4e_compress_batch_dev_dict(const uint8_t* src, const uint64_t* src_off, co
                           nblocks, max_len, dict_len};
     return hip_ok(lz4e::launch_compress(a, static_cast<hipStream_t>(stream)), "compress launch") ? 0
                                                                                                   : -1;
+}
+
+// Diagnostic (not part of include/lz4e.h): lz4e_decompress_batch_dev_dict
+// with a forced decoder (modes as lz4e_debug_decompress_stamped).
+int lz4e_debug_decompress_dict(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,
+                               uint8_t* dst, const uint64_t* dst_off, const int32_t* dst_cap, int32_t* ret,
+                               uint32_t nblocks, uint32_t max_cap, const int32_t* dict_len, void* stream,
+                               uint32_t mode) {
+    if (mode != lz4e::kDecAuto && mode != lz4e::kDecWave && mode != lz4e::kDecPipe && mode != lz4e::kDecSmall &&
+        mode != lz4e::kDecGroup && mode != lz4e::kDecGroupNoBail)
+        return -1;
+    g_err.clear();
+    lz4e::DecompressBatch a{src, src_off, src_len, dst, dst_off, dst_cap, ret, nblocks, max_cap, mode, dict_len};
+    return hip_ok(lz4e::launch_decompress(a, static_cast<hipStream_t>(stream)), "decompress launch")
+               ? 0
+               : -1;
 }
 
 int lz4e_decompress_batch_dev_dict(const uint8_t* src, const uint64_t* src_off, const int32_t* src_len,

@@ -152,6 +152,12 @@ LZ4E_DEV uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t r) {
 }
 // s_memtime: shader clock (diagnostic builds only).
 LZ4E_DEV uint64_t clock64() { return __builtin_amdgcn_s_memtime(); }
+// s_memrealtime: the constant 100 MHz clock (diagnostic builds only).
+#ifndef LZ4E_EMU
+LZ4E_DEV uint64_t realtime64() { return __builtin_amdgcn_s_memrealtime(); }
+#else
+inline uint64_t realtime64() { return 0; }
+#endif
 #ifndef LZ4E_EMU
 // Order this wave's LDS/global accesses (memory model fence, wavefront scope).
 LZ4E_DEV void wave_fence() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }

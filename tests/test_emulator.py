@@ -257,6 +257,71 @@ def test_emulated_lane_decoder_sanitized(emu_exe, tmp_path, kind, mode):
             assert got[1] == want[1], rep
 
 
+def _periodic_block(rng, periods, reps=(1, 2, 3, 17)):
+    """Self-overlapping matches of every period in `periods` at lengths around
+    1x-17x the period, separated by random bytes (the overlap-copy cases)."""
+    parts = []
+    for period in periods:
+        for rep in reps:
+            parts.append(rng.integers(0, 256, 37, dtype=np.uint8).tobytes())
+            unit = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
+            parts.append((unit * (rep + 2))[:period * rep + int(rng.integers(0, period))])
+    return b"".join(parts) + rng.integers(0, 256, 20, dtype=np.uint8).tobytes()
+
+
+NOBAIL_CASES = [(k, m) for k in ("text", "fio", "head") for m in range(5)] + \
+               [("periodic", 0), ("periodic", 3), ("periodic_dict", 0), ("periodic_dict", 1), ("periodic_dict", 4)]
+
+
+@pytest.mark.parametrize("kind,mode", NOBAIL_CASES, ids=[f"{k}-{m}" for k, m in NOBAIL_CASES])
+def test_emulated_group_decoder_no_handover(emu_exe, tmp_path, kind, mode):
+    """The group decoder with its hand-over disabled (-G, kDecGroupNoBail):
+    its own copies run on every block -- text and "head" blocks of short
+    sequences that the hand-over would give away, the period-from-registers
+    path for offsets 2-15, offset doubling from 16 on, and (periodic_dict)
+    matches that start in the dictionary and run on into the block.  Valid
+    frames (mode 0), truncations (1), bit flips (2), short capacity (3) and a
+    shortened dictionary (4) equal the oracle."""
+    rng = np.random.default_rng(900 + mode + 11 * len(kind))
+    for rep in range(2):
+        dic = b""
+        if kind.startswith("periodic"):
+            blk = _periodic_block(rng, range(2 + rep, 41, 2))
+            if kind == "periodic_dict":
+                dic = rng.integers(0, 256, 9000, dtype=np.uint8).tobytes()
+                # the block opens with the dictionary's tail, repeated: its
+                # first matches start in the dictionary and cross into the block
+                blk = (dic[-300:] * 3)[:700] + dic[-40:] + blk
+        else:
+            n = int(rng.choice([4096, int(rng.integers(13, 12000))]))
+            if kind == "fio":
+                blk = corpus.fio_pattern(16 * 4096)[(rep + 2) * 4096:][:n].tobytes()
+            elif kind == "head":
+                t = _block("text", n, 5 + rep).tobytes()
+                r = np.random.default_rng(rep).integers(0, 256, 230, dtype=np.uint8).tobytes() + bytes(200)
+                blk = (r + t)[:n]
+            else:
+                blk = _block(kind, n, 21 + rep + n).tobytes()
+        f = oracle_ref.compress_dict(blk, dic)[1] if dic else oracle_ref.compress(blk, BYU16)[1]
+        cap = len(blk)
+        if mode == 1:
+            f = f[:int(rng.integers(1, len(f)))]
+        elif mode == 2:
+            fb = bytearray(f)
+            for _ in range(3):
+                fb[int(rng.integers(0, len(fb)))] ^= 1 << int(rng.integers(0, 8))
+            f = bytes(fb)
+        elif mode == 3:
+            cap = max(0, len(blk) - int(rng.integers(1, 40)))
+        elif mode == 4 and dic:
+            dic = dic[int(rng.integers(1, 200)):]
+        want = oracle_ref.decompress_dict(f, cap, dic)
+        got = _emu_decode(emu_exe, tmp_path, f, cap, dic, "-G")
+        assert got[0] == want[0], (rep, got[0], want[0])
+        if want[0] >= 0:
+            assert got[1] == want[1], rep
+
+
 VEC_CASES = [(k, m) for k in ("random", "runs", "text") for m in range(4)]
 
 
@@ -369,9 +434,10 @@ def test_emulated_pipe_decoder_sanitized(emu_exe, tmp_path, kind, mode, flag):
 
 @pytest.fixture(scope="session")
 def emu_exe_spin1(tmp_path_factory):
-    """The decoders built with a watchdog limit of one sleep: any wait that
-    needs a second poll gives up (LZ4E_SPIN_MAX=1)."""
-    b, exe = _build_emu(tmp_path_factory, "-DLZ4E_SPIN_MAX=1")
+    """The decoders built with a watchdog limit of one sleep and no per-byte
+    term: any wait that needs a second poll gives up (LZ4E_SPIN_MAX=1,
+    LZ4E_SPIN_BYTES_SHIFT=31)."""
+    b, exe = _build_emu(tmp_path_factory, "-DLZ4E_SPIN_MAX=1", "-DLZ4E_SPIN_BYTES_SHIFT=31")
     yield exe
     shutil.rmtree(b, ignore_errors=True)
 

@@ -73,6 +73,7 @@ def _gpu_compress(amd, blocks, ttypes, caps=None):
 
 
 DEC_AUTO, DEC_WAVE, DEC_PIPE, DEC_SMALL, DEC_GROUP = 0, 1, 2, 6, 7
+DEC_GROUP_NB = 9  # the group decoder without its hand-over (every block decoded by its group)
 
 
 def _gpu_decompress(amd, frames, caps, csizes=None, max_cap=None, mode=DEC_AUTO):
@@ -276,8 +277,8 @@ def test_decompress_batch_vs_oracle(gpu, kind):
         assert outs[i] == eo == expect[i]
 
 
-@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_PIPE, DEC_WAVE, DEC_SMALL, DEC_GROUP],
-                         ids=["auto", "pipe", "wave", "small", "group"])
+@pytest.mark.parametrize("dec", [DEC_AUTO, DEC_PIPE, DEC_WAVE, DEC_SMALL, DEC_GROUP, DEC_GROUP_NB],
+                         ids=["auto", "pipe", "wave", "small", "group", "group_nobail"])
 @pytest.mark.parametrize("mode", ["truncate", "flip", "garbage", "small_cap", "csize"])
 def test_decompress_error_codes(gpu, mode, dec):
     rng = np.random.default_rng(1234 + len(mode))
@@ -378,7 +379,7 @@ def test_full_size_roundtrip(gpu, cls, bs, kind):
         assert frames[i] == oracle_ref.compress(blocks[i], cls)[1]
 
 
-@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE], ids=["wave", "pipe"])
+@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_GROUP_NB], ids=["wave", "pipe", "group_nobail"])
 def test_decompress_huge_runs(gpu, mode):
     """Blocks whose sequences are hundreds of MiB long: a 256 MiB run of one
     byte (a single match whose length extension is ~1 MiB of 0xFF) and a
@@ -397,7 +398,50 @@ def test_decompress_huge_runs(gpu, mode):
         assert outs[i] == b, i
 
 
-@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE], ids=["wave", "pipe"])
+def test_pipe_decoder_watchdog_valid_worst_case(gpu):
+    """The pipelined decoder's watchdog (decompress_pipe_kernel, DESIGN.md §3
+    "Watchdog") on valid worst-case frames under a full-chip batch: 2 048
+    blocks of 256 KiB -- runs of one byte (one offset-1 match with a ~1 KiB
+    match-length extension), incompressible data (a ~1 KiB literal-length
+    extension), text and records -- forced onto the pipelined decoder (6
+    workgroups per CU, two rounds of them).  Every block returns the
+    oracle's value (its size), never LZ4E_DECODE_ABORTED, and its bytes."""
+    import torch
+    bs, n = 262144, 2048
+    rng = np.random.default_rng(5)
+    srcs = [b"\x5a" * bs, rng.integers(0, 256, bs, dtype=np.uint8).tobytes(),
+            _corpus("text", bs, 3).tobytes(), _corpus("mixed", bs, 4).tobytes()]
+    frames = [oracle_ref.compress(b, BYU32)[1] for b in srcs]
+    for b, f in zip(srcs, frames):
+        assert oracle_ref.decompress(f, bs) == (bs, b)
+    dev = torch.device("cuda")
+    slot = (bs + bs // 255 + 16 + 15) // 16 * 16
+    src = torch.zeros(n * slot, dtype=torch.uint8, device=dev)
+    for i in range(4):
+        src[i * slot:i * slot + len(frames[i])] = torch.frombuffer(bytearray(frames[i]), dtype=torch.uint8).to(dev)
+    for i in range(4, n):  # (block i: copy of block i % 4)
+        j = i % 4
+        src[i * slot:i * slot + len(frames[j])] = src[j * slot:j * slot + len(frames[j])]
+    soff = torch.arange(n, dtype=torch.int64, device=dev) * slot
+    clen = torch.tensor([len(frames[i % 4]) for i in range(n)], dtype=torch.int32, device=dev)
+    doff = torch.arange(n, dtype=torch.int64, device=dev) * bs
+    caps = torch.full((n,), bs, dtype=torch.int32, device=dev)
+    out = torch.zeros(n * bs + 64, dtype=torch.uint8, device=dev)
+    ret = torch.full((n,), -7777, dtype=torch.int32, device=dev)
+    L = gpu.lib()
+    P = ctypes.c_void_p
+    L.lz4e_debug_decompress_stamped.argtypes = [P] * 7 + [ctypes.c_uint32, P, P, ctypes.c_uint32, ctypes.c_uint32]
+    assert L.lz4e_debug_decompress_stamped(src.data_ptr(), soff.data_ptr(), clen.data_ptr(), out.data_ptr(),
+                                           doff.data_ptr(), caps.data_ptr(), ret.data_ptr(), n, None, None,
+                                           bs, DEC_PIPE) == 0
+    torch.cuda.synchronize()
+    assert (ret == bs).all(), ret[ret != bs][:8].tolist()
+    want = [torch.frombuffer(bytearray(b), dtype=torch.uint8).to(dev) for b in srcs]
+    for i in range(n):
+        assert torch.equal(out[i * bs:(i + 1) * bs], want[i % 4]), i
+
+
+@pytest.mark.parametrize("mode", [DEC_WAVE, DEC_PIPE, DEC_GROUP_NB], ids=["wave", "pipe", "group_nobail"])
 @pytest.mark.parametrize("cap_extra", [0, 100000])
 def test_decompress_periodic_matches(gpu, cap_extra, mode):
     """Self-overlapping matches of every period 1..40 and lengths around
@@ -877,6 +921,81 @@ def test_dict_decompress_values_and_codes(gpu, big):
     # the single-call entry point on a few of them
     for i in range(0, 48, 7):
         assert gpu.decompress_safe_using_dict(frames[i], caps[i], dicts[i]) == want[i]
+
+
+@pytest.mark.parametrize("dec", [DEC_GROUP, DEC_GROUP_NB, DEC_WAVE], ids=["group", "group_nobail", "wave"])
+def test_dict_decompress_forced_decoders(gpu, dec):
+    """A dictionary batch of small blocks through a forced decoder
+    (lz4e_debug_decompress_dict): the group decoder with and without its
+    hand-over, and the one-wave decoder.  Blocks open with a repeat of the
+    dictionary's tail, so matches start in the dictionary and cross into the
+    block; periods 2..40 exercise the group's period and doubling copies.
+    Valid frames, truncations, flips and short capacities: values and bytes
+    equal the oracle's restatement of the extDict branches
+    (lz4e_decompress.c:299-302, 339-378)."""
+    import torch
+    rng = np.random.default_rng(77 + dec)
+    pool = _corpus("mixed", 1 << 20, 29).tobytes()
+    frames, caps, dicts, want = [], [], [], []
+    for i in range(96):
+        dsize = DICT_SIZES[i % len(DICT_SIZES)]
+        s0 = int(rng.integers(dsize, len(pool) - 5000))
+        dic = pool[s0 - dsize:s0]
+        per = bytearray()
+        for period in range(2 + i % 3, 41, 3):
+            unit = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
+            per += rng.integers(0, 256, 23, dtype=np.uint8).tobytes() + (unit * 9)[:period * int(rng.integers(1, 8))]
+        blk = ((dic[-200:] * 3)[:int(rng.integers(20, 600))] if dic else b"") + bytes(per) + pool[s0:s0 + 300]
+        blk = blk[:4096]
+        f = oracle_ref.compress_dict(blk, dic)[1]
+        cap = len(blk)
+        if i % 5 == 2 and len(f) > 2:
+            f = f[:int(rng.integers(1, len(f)))]
+        elif i % 5 == 3 and len(f) > 0:
+            fb = bytearray(f)
+            for _ in range(3):
+                fb[int(rng.integers(0, len(fb)))] ^= 1 << int(rng.integers(0, 8))
+            f = bytes(fb)
+        elif i % 5 == 4:
+            cap = max(0, len(blk) - int(rng.integers(1, 64)))
+        frames.append(f)
+        caps.append(cap)
+        dicts.append(dic)
+        want.append(oracle_ref.decompress_dict(f, cap, dic))
+    # device layout: [dictionary | output capacity] per block, frames packed
+    dev = torch.device("cuda")
+    n = len(frames)
+    soffs = np.concatenate([[0], np.cumsum([(len(f) + 15) // 16 * 16 for f in frames])[:-1]]).astype(np.int64)
+    src = np.zeros(int(soffs[-1]) + len(frames[-1]) + 16, np.uint8)
+    for i, f in enumerate(frames):
+        src[soffs[i]:soffs[i] + len(f)] = np.frombuffer(f, np.uint8)
+    doffs, pos = [], 0
+    for i in range(n):
+        pos += (len(dicts[i]) + 15) // 16 * 16
+        doffs.append(pos)
+        pos += (max(caps[i], 1) + 79) // 16 * 16
+    out = np.zeros(pos + 64, np.uint8)
+    for i in range(n):
+        if dicts[i]:
+            out[doffs[i] - len(dicts[i]):doffs[i]] = np.frombuffer(dicts[i], np.uint8)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a).astype(dt)).to(dev)
+    d_out = t(out, np.uint8)
+    ret = torch.full((n,), -7777, dtype=torch.int32, device=dev)
+    L = gpu.lib()
+    P = ctypes.c_void_p
+    L.lz4e_debug_decompress_dict.argtypes = [P] * 7 + [ctypes.c_uint32, ctypes.c_uint32, P, P, ctypes.c_uint32]
+    a = [t(src, np.uint8), t(soffs, np.int64), t([len(f) for f in frames], np.int32), t(doffs, np.int64),
+         t(caps, np.int32), t([len(d) for d in dicts], np.int32)]
+    assert L.lz4e_debug_decompress_dict(a[0].data_ptr(), a[1].data_ptr(), a[2].data_ptr(), d_out.data_ptr(),
+                                        a[3].data_ptr(), a[4].data_ptr(), ret.data_ptr(), n, max(caps),
+                                        a[5].data_ptr(), None, dec) == 0
+    torch.cuda.synchronize()
+    r = ret.cpu().numpy()
+    o = d_out.cpu().numpy()
+    for i, (er, eb) in enumerate(want):
+        assert r[i] == er, (i, r[i], er)
+        if er >= 0:
+            assert o[doffs[i]:doffs[i] + er].tobytes() == eb, i
 
 
 def test_dict_streams_device_resident(gpu):

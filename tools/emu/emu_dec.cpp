@@ -17,7 +17,8 @@
 
 // Block i decodes src_len[i] bytes at src + src_off[i] into dst + dst_off[i]
 // (capacity dst_cap[i]), dictionary: the dict_len[i] bytes before it
-// (dict_len nullable).  mode: 1 one-wave decoder, 2 pipelined decoder.
+// (dict_len nullable).  mode: 1 one-wave decoder, 2 pipelined decoder, 6 LDS form,
+// 7 group decoder, 9 group decoder without the hand-over.
 extern "C" int emu_decompress_batch_mode(const uint8_t* src, const uint64_t* src_off,
                                          const int32_t* src_len, uint8_t* dst, const uint64_t* dst_off,
                                          const int32_t* dst_cap, int32_t* ret, uint32_t nblocks,

@@ -7,6 +7,8 @@
 //            LDS output for blocks of <= 4608 bytes without a dictionary)
 //   emu_main -g FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (block-per-group
 //            decoder, 8 lanes a block)
+//   emu_main -G FRAME_FILE CAPACITY [OUT_FILE [DICT_FILE]]   (the same without
+//            the hand-over: every block decoded to its end by its group)
 // compresses one block through the unmodified kernel source, prints the
 // return value and the iterator post-state words, and writes the frame.
 // With DICT_FILE the block is compressed in dictionary mode against the
@@ -63,7 +65,7 @@ static int decode_main(int argc, char** argv) {
     frame.reserve((frame.size() + 3) & ~(size_t)3);
     // kDecPipe / kDecSmall / kDecGroup / kDecWave
     const char m = argv[1][1];
-    const uint32_t mode = m == 'p' ? 2u : (m == 'l' ? 6u : (m == 'g' ? 7u : 1u));
+    const uint32_t mode = m == 'p' ? 2u : (m == 'l' ? 6u : (m == 'g' ? 7u : (m == 'G' ? 9u : 1u)));
     emu_decompress_batch_mode(frame.data(), &so, &csize, out.data(), &doff, &cap, &ret, 1, &D, mode);
     char err[256];
     const int good = emu_decode_results(&ret, 1, err, sizeof err);
@@ -79,7 +81,7 @@ static int decode_main(int argc, char** argv) {
 
 int main(int argc, char** argv) {
     if (argc > 3 && argv[1][0] == '-' &&
-        (argv[1][1] == 'd' || argv[1][1] == 'p' || argv[1][1] == 'l' || argv[1][1] == 'g'))
+        (argv[1][1] == 'd' || argv[1][1] == 'p' || argv[1][1] == 'l' || argv[1][1] == 'g' || argv[1][1] == 'G'))
         return decode_main(argc, argv);
     if (argc < 3) {
         fprintf(stderr, "usage: emu_main BLOCK_FILE TABLE_CLASS [FRAME_OUT]\n");

@@ -99,6 +99,9 @@ struct EmuWave {
             for (uint32_t g = 0; g < 64 / w; ++g) groups.emplace_back(w);
     }
     EmuBarrier& group_bar(uint32_t width, uint32_t lane) {
+        // groups of 2, 4, ..., 32 lanes only (a width of 1 or 64 has no
+        // barrier here: lz4e_decompress.hip's static_assert keeps kGroup in range)
+        if (width < 2 || width > 32 || (width & (width - 1)) != 0) abort();
         uint32_t base = 0;
         for (uint32_t w = 2; w < width; w *= 2) base += 64 / w;
         return groups[base + lane / width];

@@ -44,7 +44,7 @@ def run(name, data, bs, cls, label):
     src = torch.from_numpy(data).to(dev)
     dst = torch.zeros(n * slot, dtype=torch.uint8, device=dev)
     ret = torch.zeros(n, dtype=torch.int32, device=dev)
-    dbg = torch.zeros(n * 8, dtype=torch.int64, device=dev)
+    dbg = torch.zeros(n * 16, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream().cuda_stream
     for _ in range(2):
         r = L.lz4e_debug_compress_stamped(src.data_ptr(), offs.data_ptr(), lens.data_ptr(), tt.data_ptr(),
@@ -52,7 +52,7 @@ def run(name, data, bs, cls, label):
                                           n, bs, s, dbg.data_ptr())
         assert r == 0
     torch.cuda.synchronize()
-    d = dbg.cpu().numpy().reshape(n, 8).astype(np.float64)
+    d = dbg.cpu().numpy().reshape(n, 16).astype(np.float64)
     ph = ["setup", "slowwalk", "chainwalk", "tables", "commit", "emit"]
     srch = d[:, 6].astype(np.int64) & 0xFFFFFFFF
     seqs = d[:, 6].astype(np.int64) >> 32
