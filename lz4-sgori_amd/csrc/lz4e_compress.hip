@@ -92,6 +92,13 @@ struct HbmImage {
     // fully inside); buffer loads take the constant part of the offset in
     // the instruction and merge into dwordx4.
     LZ4E_DEV uint32_t wld(uint32_t q) const { return buf_ld32(buf, q); }
+    // o[0] = the dword at q - 4, o[1 + i] = the dword at q + 4 i (i < 8)
+    LZ4E_DEV void wld9(uint32_t q, uint32_t* o) const {
+        o[0] = wld(q - 4);
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) o[1 + i] = wld(q + 4 * i);
+    }
+    static constexpr bool kInLds = false;
     LZ4E_DEV uint32_t ld32(uint32_t q) const { return buf_ld32(buf, vaddr(q)); }
     LZ4E_DEV uint64_t ld64(uint32_t q) const {
         const uint32_t v = vaddr(q);
@@ -120,6 +127,17 @@ struct LdsImage {
     }
     LZ4E_DEV uint32_t stripe(uint32_t X, uint32_t lane) const { return ld32(X - 4 + 4 * lane); }
     LZ4E_DEV uint32_t wld(uint32_t q) const { return ld32(q); }
+    // HbmImage::wld9 from 10 shared word reads (the overlapping dwords of
+    // a 36-byte run need 10 words, not 18)
+    LZ4E_DEV void wld9(uint32_t q, uint32_t* o) const {
+        const uint32_t i0 = (q >> 2) - 1, r = q & 3;  // (q < 4: the clamp, as in ld32)
+        uint32_t w[10];
+#pragma unroll
+        for (uint32_t k = 0; k < 10; ++k) w[k] = word(i0 + k);
+#pragma unroll
+        for (uint32_t k = 0; k < 9; ++k) o[k] = alignbyte(w[k + 1], w[k], r);
+    }
+    static constexpr bool kInLds = true;
 };
 
 // Phase cycle counters of the diagnostic build (launch_compress_stamped).
@@ -453,9 +471,11 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
         auto preload = [&](uint32_t Bn) {
             if (Bn == nB) return;
             nB = Bn;
-            ndm1 = img.wld(Bn + lane - 4);
+            uint32_t o[9];
+            img.wld9(Bn + lane, o);
+            ndm1 = o[0];
 #pragma unroll
-            for (uint32_t i = 0; i < kFwdW; ++i) ndv[i] = img.wld(Bn + lane + 4 * i);
+            for (uint32_t i = 0; i < kFwdW; ++i) ndv[i] = o[1 + i];
         };
         for (;;) {
             // ================= window setup =================================
@@ -474,20 +494,31 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
 #pragma unroll
                 for (uint32_t i = 0; i < kFwdW; ++i) dv[i] = ndv[i];
             } else {
-                dm1 = img.wld(p - 4);
+                uint32_t o[9];
+                img.wld9(p, o);
+                dm1 = o[0];
 #pragma unroll
-                for (uint32_t i = 0; i < kFwdW; ++i) dv[i] = img.wld(p + 4 * i);
+                for (uint32_t i = 0; i < kFwdW; ++i) dv[i] = o[1 + i];
             }
             const uint32_t d0 = dv[0];
             const uint32_t h = hash_val<TT>(((uint64_t)dv[1] << 32) | d0);
             uint32_t c0 = 0, rb = p;
             lockstep();  // the previous window's commit is in the table
             if (valid) c0 = T.get(h);  // snapshot
-            // the snapshot candidate's bytes: issued now, used after the clash groups
-            const uint32_t em1 = img.wld(c0 - 4);
-            uint32_t ev[kFwdW];
+            // the snapshot candidate's bytes: issued now, used after the clash
+            // groups (a block staged in LDS: only the first dword, the rest
+            // when some lane's first 4 bytes match -- windows of
+            // incompressible data need none of them)
+            uint32_t em1 = 0, ev[kFwdW];
+            if constexpr (!IMG::kInLds) {
+                uint32_t o[9];
+                img.wld9(c0, o);
+                em1 = o[0];
 #pragma unroll
-            for (uint32_t i = 0; i < kFwdW; ++i) ev[i] = img.wld(c0 + 4 * i);
+                for (uint32_t i = 0; i < kFwdW; ++i) ev[i] = o[1 + i];
+            } else {
+                ev[0] = img.wld(c0);
+            }
             lockstep();
             if (valid) T.put(h, p);  // speculative put of every position
             lockstep();
@@ -507,8 +538,23 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
             uint32_t ml = 0, bk = kNoBk;
             {
                 const bool dist_ok = (TT == kByU16) || (c0 + kMaxDistance >= p);
-                if (valid && dist_ok) ml = fwd_match(dv, ev, lim);
-                if (p >= 4 && c0 >= 4) bk = back4(dm1, em1);
+                // (LDS image: no lane's first dword verifying leaves ml = 0
+                // everywhere -- fwd_match's result -- and bk unused)
+                bool full = true;
+                if constexpr (IMG::kInLds) {
+                    full = ballot(valid && dist_ok && ev[0] == d0) != 0;
+                    if (full) {
+                        uint32_t o[9];
+                        img.wld9(c0, o);
+                        em1 = o[0];
+#pragma unroll
+                        for (uint32_t i = 1; i < kFwdW; ++i) ev[i] = o[1 + i];
+                    }
+                }
+                if (full) {
+                    if (valid && dist_ok) ml = fwd_match(dv, ev, lim);
+                    if (p >= 4 && c0 >= 4) bk = back4(dm1, em1);
+                }
             }
             const uint64_t hitm = ballot(ml != 0);
             uint64_t put = 0;
@@ -578,7 +624,7 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
             // the next window starts at or a little after B + 64: touch
             // [B + 64, B + 320) now, one dword per lane, so that its loads hit
             // cache (the value is only kept alive, never used)
-            pf = img.wld(B + 64 + 4 * lane);
+            if constexpr (!IMG::kInLds) pf = img.wld(B + 64 + 4 * lane);
             if (kStamps) { st.cnt[0]++; st.lap(kPhSearch); }
 
             // ================= walk =========================================

@@ -49,4 +49,5 @@ if __name__ == "__main__":
     print("==", tag)
     run("silesia64k", corpus.silesia_proxy(3234 * 65536, 0x5157), 65536)
     run("text64k", corpus.text_proxy(1024 * 65536, 7), 65536)
-    run("fio4k", corpus.fio_pattern(16384 * 4096), 4096)
+    run("fio4k", corpus.fio_pattern(262144 * 4096), 4096)
+    run("text4k", corpus.text_proxy(16384 * 4096, 9), 4096)
