@@ -330,8 +330,8 @@ int lz4e_decompress_sg_batch(const char *const *src, const int *csize,
  * that frame back into the chunk's contiguous source buffer, whose size must
  * equal the bio's, lz4e_chunk.c:133).  Requests flow through four pipeline
  * slots (pinned staging + HBM buffers + a HIP stream each) in sub-batches of
- * up to 64 MiB: the SG gather of one sub-batch overlaps the H2D copies,
- * kernels and D2H copies of the others.
+ * a quarter of the call (16-256 MiB of input): the SG gather of one
+ * sub-batch overlaps the H2D copies, kernels and D2H copies of the others.
  */
 struct lz4e_chunk_request {
 	const struct bio_vec *src;       /* original bio's bi_io_vec            */

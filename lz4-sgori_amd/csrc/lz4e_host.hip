@@ -20,6 +20,7 @@
 #include <condition_variable>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -961,28 +962,84 @@ namespace {
 
 constexpr int kEIO = -5, kENOSPC = -28;
 
-constexpr uint64_t kSubBytes = 64ull << 20;  // input bytes per pipeline sub-batch
-constexpr uint32_t kSubReqs = 16384;         // requests per sub-batch
-// Sub-batches in flight.  A sub-batch's kernels take about the slowest
-// block's parse time whatever their size, so several run side by side on
-// their own streams to keep the GPU full while the host gathers the next.
+// Sub-batch size: a kSlots-th of the call, so that every sub-batch is in
+// flight at once and the GPU sees the whole call as one batch launch would
+// (a sub-batch's kernels take at least its slowest block's parse: 64 MiB of
+// 256 KiB blocks is 256 blocks, a tenth of the chip), between these bounds
+// of input bytes; at least kSubReqsMin requests.
+constexpr uint64_t kSubBytesMin = 16ull << 20, kSubBytesMax = 256ull << 20;
+constexpr uint32_t kSubReqsMin = 16384;
+// Sub-batches in flight, each on its own stream, while the host gathers the
+// next.
 constexpr uint32_t kSlots = 4;
+
+// Persistent host threads for the pipeline's gathers and copy-outs (a
+// thread per worker and job cost ~1 ms per sub-batch).  One job at a time:
+// the caller holds the chunk context's lock.
+class HostPool {
+  public:
+    explicit HostPool(uint32_t workers) {
+        for (uint32_t w = 0; w < workers; ++w) th_.emplace_back([this, w] { loop(w + 1); });
+    }
+    uint32_t size() const { return (uint32_t)th_.size() + 1; }
+    // f(t) for t in [0, T) (T <= size()); the caller runs f(0)
+    void run(uint32_t T, const std::function<void(uint32_t)>& f) {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            job_ = &f;
+            active_ = T;
+            pending_ = T - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return pending_ == 0; });
+    }
+
+  private:
+    void loop(uint32_t t) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(uint32_t)>* j;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (t >= active_) continue;
+                j = job_;
+            }
+            (*j)(t);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> th_;
+    const std::function<void(uint32_t)>* job_ = nullptr;
+    uint32_t active_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+};
+
+HostPool& host_pool() {
+    // never destroyed: its threads wait for jobs until the process ends
+    static HostPool* p = new HostPool(std::min(16u, std::max(1u, std::thread::hardware_concurrency())) - 1);
+    return *p;
+}
 
 // Runs f(j) for j in [0, n) on up to 16 host threads when the bytes justify it.
 template <class F>
 void par_for(uint32_t n, uint64_t bytes, F f) {
-    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
-    const uint32_t T = bytes < (4ull << 20) ? 1u : std::min({16u, hw, n});
+    const uint32_t T = bytes < (4ull << 20) ? 1u : std::min(host_pool().size(), n);
     if (T <= 1) {
         for (uint32_t j = 0; j < n; ++j) f(j);
         return;
     }
-    std::vector<std::thread> th;
-    for (uint32_t t = 0; t < T; ++t)
-        th.emplace_back([&, t] {
-            for (uint32_t j = t; j < n; j += T) f(j);
-        });
-    for (auto& x : th) x.join();
+    const std::function<void(uint32_t)> job = [&](uint32_t t) {
+        for (uint32_t j = t; j < n; j += T) f(j);
+    };
+    host_pool().run(T, job);
 }
 
 // Per-sub-batch metadata (device + pinned host), one entry per request.
@@ -1086,6 +1143,10 @@ uint64_t bio_vcnt_of_buffer(const char* data, uint32_t len) {
 // after this many sub-batches have been submitted (-1: never).
 std::atomic<int> g_chunk_fault_after{-1};
 
+// Debug hook (tests only): sub-batches of this many input bytes instead of
+// the call-sized ones (0: off), so that a small call cycles the slots.
+std::atomic<uint64_t> g_chunk_sub_bytes{0};
+
 // Launch order override per direction (compress, decompress): -1 default.
 std::atomic<int> g_order_override[2] = {{-1}, {-1}};
 
@@ -1176,6 +1237,7 @@ int launch_order_mode(bool compress) {
 extern "C" {
 
 void lz4e_debug_chunk_fault_after(int subbatches) { g_chunk_fault_after.store(subbatches); }
+void lz4e_debug_chunk_sub_bytes(uint64_t bytes) { g_chunk_sub_bytes.store(bytes); }
 
 // Diagnostic: launch order policy of the device batches (lz4e_order.h) for
 // compress / decompress: -1 default (environment), 0 block order, 1 heavy
@@ -1212,6 +1274,12 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
         chunk_drain(cc);
         return fail_all();
     };
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < N; ++r) total += reqs[r].srcIter->bi_size;
+    const uint64_t forced = g_chunk_sub_bytes.load();
+    const uint64_t sub_bytes =
+        forced ? forced : std::min(kSubBytesMax, std::max(kSubBytesMin, (total + kSlots - 1) / kSlots));
+    const uint32_t sub_reqs = forced ? kSubReqsMin : std::max(kSubReqsMin, (N + kSlots - 1) / kSlots);
     while (i < N) {
         ChunkSlot& s = cc.slot[k % kSlots];
         if (!chunk_finish(s, reqs, st, good, pr)) return abort();
@@ -1229,7 +1297,7 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
         uint64_t ib = 0, fb = 0, ob = 0;
         uint32_t max_len = 0;
         bool frames = false;
-        for (; i < N && s.req.size() < kSubReqs && (s.req.empty() || ib < kSubBytes); ++i) {
+        for (; i < N && s.req.size() < sub_reqs && (s.req.empty() || ib < sub_bytes); ++i) {
             const lz4e_chunk_request& q = reqs[i];
             const uint32_t len = q.srcIter->bi_size;
             int t = LZ4E_TABLE_BYU16;

@@ -519,7 +519,10 @@ def test_chunk_write_batch_layouts(gpu):
 
 
 def test_chunk_write_batch_streamed(gpu):
-    """More input than one 64 MiB pipeline sub-batch: the slots cycle."""
+    """144 MiB of input through the pipeline twice: in 16 MiB sub-batches
+    (nine, so the four slots cycle: a slot's results are handed out before
+    it takes the next sub-batch) and in the default call-sized ones (four,
+    all in flight together)."""
     bs, nreq = 65536, 2200
     data = corpus.silesia_proxy(nreq * bs, 0x5157)
     srcs, payloads = [], []
@@ -527,14 +530,21 @@ def test_chunk_write_batch_streamed(gpu):
         blk = data[i * bs:(i + 1) * bs].tobytes()
         srcs.append(make_sg(blk, [4096] * 16))
         payloads.append(blk)
-    stats = gpu.ChunkStats()
-    good, res = gpu.chunk_write_batch(srcs, want_frames=True, stats=stats)
-    assert good == nreq and stats.reqs_failed == 0
-    assert all(st == 0 and d == b for (st, _, d, _), b in zip(res, payloads))
-    for i in range(0, nreq, 157):
-        er, ef, _, _ = oracle_ref.compress(payloads[i], BYU16)
-        assert res[i][1] == er and res[i][3] == ef
-    assert stats.frame_bytes == sum(r[1] for r in res)
+    L = gpu.lib()
+    L.lz4e_debug_chunk_sub_bytes.argtypes = [ctypes.c_uint64]
+    for sub in (16 << 20, 0):
+        L.lz4e_debug_chunk_sub_bytes(sub)
+        try:
+            stats = gpu.ChunkStats()
+            good, res = gpu.chunk_write_batch(srcs, want_frames=True, stats=stats)
+        finally:
+            L.lz4e_debug_chunk_sub_bytes(0)
+        assert good == nreq and stats.reqs_failed == 0
+        assert all(st == 0 and d == b for (st, _, d, _), b in zip(res, payloads))
+        for i in range(0, nreq, 157):
+            er, ef, _, _ = oracle_ref.compress(payloads[i], BYU16)
+            assert res[i][1] == er and res[i][3] == ef
+        assert stats.frame_bytes == sum(r[1] for r in res)
 
 
 # ---------------------------------------------------------------------------
@@ -604,7 +614,7 @@ def test_chunk_write_batch_fault_then_smaller_call(gpu):
     sub-batch is in flight) returns -1 with every request -EIO and the
     caller's stats untouched; the next, smaller call is unaffected by what
     the failed one left in flight."""
-    bs, nreq = 65536, 1100  # two 64 MiB sub-batches
+    bs, nreq = 65536, 1100  # four 18 MiB sub-batches
     data = corpus.silesia_proxy(nreq * bs, 77)
     srcs = [make_sg(data[i * bs:(i + 1) * bs].tobytes(), [4096] * 16) for i in range(nreq)]
     L = gpu.lib()
