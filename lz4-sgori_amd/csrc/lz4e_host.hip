@@ -1072,6 +1072,11 @@ struct ChunkSlot {
     std::vector<uint64_t> fr, out;    // frame / output offsets in the data buffer
     uint64_t in_bytes = 0, fr_bytes = 0, out_bytes = 0;
     size_t meta_ret = 0, meta_dret = 0;
+    // LZ4E_CHUNK_PROF=2: timing events (before H2D, after H2D, compress,
+    // decompress, D2H) and host times of the sub-batch's phases
+    hipEvent_t pev[5] = {};
+    uint32_t sb = 0;
+    double t_g0 = 0, t_g1 = 0, t_sub = 0;
 };
 
 struct ChunkCtx {
@@ -1112,6 +1117,8 @@ double now_ms() {
 }
 struct ChunkProf {
     bool on = getenv("LZ4E_CHUNK_PROF") != nullptr;
+    bool tl = on && getenv("LZ4E_CHUNK_PROF")[0] == '2';  // per-sub-batch timeline
+    double t0 = 0;
     double wait = 0, out = 0, gather = 0, submit = 0;
 };
 
@@ -1191,6 +1198,14 @@ bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chu
         q.status = 0;
     });
     if (pr.on) pr.out += now_ms() - t1;
+    if (pr.tl && s.pev[4]) {
+        float g[4] = {0, 0, 0, 0};
+        for (int q = 0; q < 4; ++q) (void)hipEventElapsedTime(&g[q], s.pev[q], s.pev[q + 1]);
+        fprintf(stderr, "  sb %u: %u reqs, gather %.2f-%.2f, submitted %.2f, waited %.2f-%.2f, copied out by %.2f;"
+                " gpu h2d %.2f compress %.2f decompress %.2f d2h %.2f ms\n", s.sb, R, s.t_g0 - pr.t0,
+                s.t_g1 - pr.t0, s.t_sub - pr.t0, t0 - pr.t0, t1 - pr.t0, now_ms() - pr.t0, g[0], g[1],
+                g[2], g[3]);
+    }
     // Stats as the reference keeps them: lz4e_stats_update runs only in
     // lz4e_end_io (lz4e_bdev/lz4e_req.c:231-246), i.e. for a WRITE whose
     // round trip succeeded and whose bio was submitted; a request failing in
@@ -1217,7 +1232,8 @@ bool chunk_finish(ChunkSlot& s, struct lz4e_chunk_request* reqs, struct lz4e_chu
 void chunk_drain(ChunkCtx& cc) {
     for (uint32_t t = 0; t < kSlots; ++t) {
         ChunkSlot& s = cc.slot[t];
-        if (s.busy) (void)hipEventSynchronize(s.done);
+        // (the failure may have come before `done` was recorded)
+        if (s.busy) (void)hipStreamSynchronize(s.stream);
         s.busy = false;
         s.req.clear();
     }
@@ -1270,6 +1286,7 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
     const uint32_t N = (uint32_t)n;
     ChunkProf pr;
     const double tstart = pr.on ? now_ms() : 0;
+    pr.t0 = tstart;
     auto abort = [&]() {
         chunk_drain(cc);
         return fail_all();
@@ -1341,6 +1358,16 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
         });
         const double ts = pr.on ? now_ms() : 0;
         pr.gather += ts - tg;
+        if (pr.tl) {
+            for (hipEvent_t& ev : s.pev)
+                if (!ev && hipEventCreate(&ev) != hipSuccess) ev = nullptr;
+            s.sb = k;
+            s.t_g0 = tg;
+            s.t_g1 = ts;
+        }
+        auto mark = [&](int q) {
+            if (pr.tl && s.pev[q]) (void)hipEventRecord(s.pev[q], s.stream);
+        };
         for (uint32_t j = 0; j < R; ++j) {
             const uint32_t len = reqs[s.req[j]].srcIter->bi_size;
             reinterpret_cast<uint64_t*>(hm + m.in_off)[j] = in[j];
@@ -1378,16 +1405,23 @@ int lz4e_chunk_write_batch(struct lz4e_chunk_request* reqs, int n, struct lz4e_c
                                        max_len};
         // from here on the slot has work in flight: a failure must drain it
         s.busy = true;
+        mark(0);
         if (!hip_ok(hipMemcpyAsync(dd, hd, ib, hipMemcpyHostToDevice, s.stream), "H2D data") ||
-            !hip_ok(hipMemcpyAsync(dm, hm, m.ret, hipMemcpyHostToDevice, s.stream), "H2D meta") ||
-            !hip_ok(lz4e::launch_compress(ca, s.stream), "compress launch") ||
-            !hip_ok(lz4e::launch_decompress(da, s.stream), "decompress launch") ||
-            !hip_ok(hipMemcpyAsync(hm + m.ret, dm + m.ret, m.total - m.ret, hipMemcpyDeviceToHost,
+            !hip_ok(hipMemcpyAsync(dm, hm, m.ret, hipMemcpyHostToDevice, s.stream), "H2D meta"))
+            return abort();
+        mark(1);
+        if (!hip_ok(lz4e::launch_compress(ca, s.stream), "compress launch")) return abort();
+        mark(2);
+        if (!hip_ok(lz4e::launch_decompress(da, s.stream), "decompress launch")) return abort();
+        mark(3);
+        if (!hip_ok(hipMemcpyAsync(hm + m.ret, dm + m.ret, m.total - m.ret, hipMemcpyDeviceToHost,
                                    s.stream), "D2H meta") ||
             (frames && !hip_ok(copy_flat(s.h_dev, dd, ib, fb, s.stream), "D2H frames")) ||
-            !hip_ok(copy_flat(s.h_dev, dd, ib + fb, ob, s.stream), "D2H data") ||
-            !hip_ok(hipEventRecord(s.done, s.stream), "event record"))
+            !hip_ok(copy_flat(s.h_dev, dd, ib + fb, ob, s.stream), "D2H data"))
             return abort();
+        mark(4);
+        if (!hip_ok(hipEventRecord(s.done, s.stream), "event record")) return abort();
+        s.t_sub = pr.on ? now_ms() : 0;
         k++;
         if (pr.on) pr.submit += now_ms() - ts;
     }
