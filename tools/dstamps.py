@@ -1,4 +1,6 @@
-"""Diagnostic: per-phase cycles of the decompress kernel (stamped build)."""
+"""Diagnostic: per-phase cycles of the one-wave decompress kernel (stamped build).
+
+usage: python tools/dstamps.py [silesia64k,text64k,fio4k,text256k,text256k_16]"""
 import ctypes, os, sys
 import numpy as np
 
@@ -52,6 +54,11 @@ def run(name, data, bs, cls):
           f"lit {d[:,1].mean():.0f} match {d[:,2].mean():.0f} flush {d[:,5].mean():.0f}; cycles/batch {tot.sum()/max(1,d[:,3].sum()):.0f}")
     by_class(name, tot, n, lambda m: f"batches {d[m,3].mean():.0f} rounds {d[m,4].mean():.0f} parse {d[m,0].mean():.0f} lit {d[m,1].mean():.0f} match {d[m,2].mean():.0f}")
 
-run("silesia64k", corpus.silesia_proxy(1024 * 65536, 0x5157), 65536, 1)
-run("text64k", corpus.text_proxy(512 * 65536, 7), 65536, 1)
-run("fio4k", corpus.fio_pattern(16384 * 4096), 4096, 1)
+W = {"silesia64k": lambda: (corpus.silesia_proxy(1024 * 65536, 0x5157), 65536, 1),
+     "text64k": lambda: (corpus.text_proxy(512 * 65536, 7), 65536, 1),
+     "fio4k": lambda: (corpus.fio_pattern(16384 * 4096), 4096, 1),
+     # configs[4]'s decompress-only leg (one wave per block), full chip and 16 blocks
+     "text256k": lambda: (corpus.text_proxy(3815 * 262144, 7), 262144, 3),
+     "text256k_16": lambda: (corpus.text_proxy(16 * 262144, 7), 262144, 3)}
+for name in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["silesia64k", "text64k", "fio4k"]):
+    run(name, *W[name]())
