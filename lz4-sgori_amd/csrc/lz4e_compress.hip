@@ -390,6 +390,14 @@ struct CResult {
     int32_t ret = 0;
     uint32_t a0 = 0, a1 = 0;
 };
+// Probes done (of a search that missed through its window) from which the
+// generic search takes over (LZ4E_GENERIC_FROM, experiments; 64: only for
+// skip steps > 1).
+#ifndef LZ4E_GENERIC_FROM
+#define LZ4E_GENERIC_FROM 48
+#endif
+constexpr uint32_t kGenericFrom = LZ4E_GENERIC_FROM;
+
 template <int TT, bool kStamps, class IMG>
 LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8* out, uint32_t cap,
                                 uint64_t* dbg, uint32_t lane, uint32_t D = 0, bool progress_prio = true) {
@@ -866,7 +874,13 @@ LZ4E_DEV CResult compress_block(const IMG& img, uint32_t* smem, uint32_t n, gu8*
                         ip = B + lastv;
                         goto last_literals;
                     }
-                    if (jb > 64) {  // skip steps > 1 from here: generic search
+                    // Skip steps > 1 from probe 65 on, and then the generic
+                    // search.  It also takes the search over once fewer than
+                    // 64 - kGenericFrom step-1 probes are left: a window for
+                    // those few lanes costs a whole setup and commit (fio's
+                    // incompressible runs: the search misses through the
+                    // first window, then three or four probes in a second).
+                    if (jb > kGenericFrom) {
                         generic = true;
                         break;
                     }
