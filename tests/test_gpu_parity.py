@@ -194,6 +194,32 @@ def test_compress_batch_vs_oracle(gpu, kind, cls):
         assert (aux[i][0], aux[i][1]) == (efs, elr), (i, len(b))
 
 
+@pytest.mark.parametrize("cls", [BYU16, BYU32])
+def test_compress_search_handover_patterns(gpu, cls):
+    """Blocks of [R random bytes | Z equal bytes] chunks: after each match the
+    rematch misses and the search runs through its window, hands over to the
+    generic skip-step search at probe 48 and finds the next run at a probe
+    number set by R -- before, at and after the hand-over, with the block end
+    (mflimit) landing inside the search for the truncated lengths.  LDS-staged
+    (<= 4 KiB) and HBM blocks; frames, sizes and iterator post-state equal the
+    oracle's."""
+    rng = np.random.default_rng(4801 + cls)
+    blocks = []
+    for R in (20, 40, 47, 48, 49, 55, 60, 64, 66, 70, 100, 130, 200, 300):
+        for Z in (13, 64, 256):
+            unit = np.concatenate([rng.integers(0, 256, R, dtype=np.uint8), np.full(Z, 7, np.uint8)])
+            data = np.tile(unit, 65536 // unit.size + 2)
+            for ln in (4096, 4095, 3000, 2500, 20000, 65536):
+                if cls == BYU16 or ln != 4095:
+                    blocks.append(data[:ln].tobytes())
+    r, frames, aux = _gpu_compress(gpu, blocks, [cls] * len(blocks))
+    for i, b in enumerate(blocks):
+        er, ef, efs, elr = oracle_ref.compress(b, cls)
+        assert r[i] == er, (i, len(b))
+        assert frames[i] == ef, (i, len(b))
+        assert (aux[i][0], aux[i][1]) == (efs, elr), (i, len(b))
+
+
 def test_compress_byu64(gpu):
     """byU64 class (a > 16 MiB segment): HBM-resident path, 2048-entry table."""
     n = (1 << 24) + 40000
