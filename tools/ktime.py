@@ -12,12 +12,12 @@ import lz4e_amd  # noqa
 from lz4e_amd import corpus  # noqa
 
 
-def run(name, data, bs, reps=5):
+def run(name, data, bs, reps=5, cls=None):
     dev = torch.device("cuda")
     n = data.size // bs
     offs = torch.arange(n, dtype=torch.int64, device=dev) * bs
     lens = torch.full((n,), bs, dtype=torch.int32, device=dev)
-    tt = torch.full((n,), 1 if bs <= 65536 else 3, dtype=torch.uint8, device=dev)
+    tt = torch.full((n,), cls or (1 if bs <= 65536 else 3), dtype=torch.uint8, device=dev)
     cap = bs + bs // 255 + 16
     slot = (cap + 79) // 16 * 16
     doffs = torch.arange(n, dtype=torch.int64, device=dev) * slot
@@ -48,6 +48,8 @@ if __name__ == "__main__":
     tag = os.environ.get("LZ4E_LIB", "default")
     print("==", tag)
     run("silesia64k", corpus.silesia_proxy(3234 * 65536, 0x5157), 65536)
+    if os.environ.get("KTIME_U32"):  # the sg512 workload's table class
+        run("silesia64k-u32", corpus.silesia_proxy(3234 * 65536, 0x5157), 65536, cls=3)
     run("text64k", corpus.text_proxy(1024 * 65536, 7), 65536)
     run("fio4k", corpus.fio_pattern(262144 * 4096), 4096)
     run("text4k", corpus.text_proxy(16384 * 4096, 9), 4096)
