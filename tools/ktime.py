@@ -48,6 +48,8 @@ if __name__ == "__main__":
     tag = os.environ.get("LZ4E_LIB", "default")
     print("==", tag)
     run("silesia64k", corpus.silesia_proxy(3234 * 65536, 0x5157), 65536)
+    if os.environ.get("KTIME_T256"):  # configs[4]: 3 815 blocks of 256 KiB (byU32), issue-bound
+        run("text256k", corpus.text_proxy(3815 * 262144, 7), 262144)
     if os.environ.get("KTIME_U32"):  # the sg512 workload's table class
         run("silesia64k-u32", corpus.silesia_proxy(3234 * 65536, 0x5157), 65536, cls=3)
     run("text64k", corpus.text_proxy(1024 * 65536, 7), 65536)
