@@ -1696,7 +1696,7 @@ __global__ __launch_bounds__(64) void decompress_resume_kernel(
 // poll one word instead of three and were 10 % faster on silesia64k.  Every
 // wait is bounded (watchdog).
 // LZ4E_PIPE_WAVES: workgroup size of the pipelined decoder (parser + copiers;
-// experiments only -- 3 and 5 waves measured slower than 4).
+// experiments only -- 2, 3 and 5 waves measured slower than 4).
 #ifndef LZ4E_PIPE_WAVES
 #define LZ4E_PIPE_WAVES 4
 #endif
